@@ -1,0 +1,114 @@
+"""ctypes mirror of ``include/gw_engine.h`` (constants and config structs).
+
+Only plain C types cross the boundary: the engine takes device pointers as
+integers (``tensor.data_ptr()``) and streams as ``void*``.
+"""
+import ctypes as C
+
+GW_MAX_AGENTS = 64
+GW_MAX_ENC = 15
+GW_MAX_CELLS = 4096
+GW_MAX_RANGE = 7
+GW_ACT_DIM = 3
+GW_MT_N = 624
+GW_MT_STRIDE = 640
+
+GW_OK = 0
+GW_E_INVALID = -1
+GW_E_HIP = -2
+GW_E_UNSUPPORTED = -3
+
+GW_ERR_NO_CELL = 1
+GW_ERR_INIT_POSITION = 2
+
+GW_K_OBSERVING = 0x01
+GW_K_ACTING = 0x02
+GW_K_GRID_OBSERVER = 0x04
+GW_K_MOVING = 0x08
+GW_K_ATTACKING = 0x10
+GW_K_HEALTH = 0x20
+GW_K_BLOCKING = 0x40
+
+GW_SIM_TEAM_BATTLE = 1
+GW_SIM_MAZE_NAV = 2
+
+GW_DONE_ACTIVE = 0x1
+GW_DONE_ONE_TEAM = 0x2
+
+GW_ORDER_POSITION_HEALTH = 0
+GW_ORDER_HEALTH_POSITION = 1
+
+# flags bits in gw_get_state
+FLAG_IN_GRID = 1
+FLAG_LIVE = 2
+FLAG_ACTIVE = 4
+
+
+class AgentSpec(C.Structure):
+    _fields_ = [
+        ("encoding", C.c_int32),
+        ("kind", C.c_uint32),
+        ("init_row", C.c_int32),
+        ("init_col", C.c_int32),
+        ("view_range", C.c_int32),
+        ("move_range", C.c_int32),
+        ("attack_range", C.c_int32),
+        ("simultaneous_attacks", C.c_int32),
+        ("attack_strength", C.c_double),
+        ("attack_accuracy", C.c_double),
+        ("initial_health", C.c_double),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("rows", C.c_int32),
+        ("cols", C.c_int32),
+        ("n_agents", C.c_int32),
+        ("sim_kind", C.c_int32),
+        ("overlap", C.c_uint32 * (GW_MAX_ENC + 1)),
+        ("attack_mapping", C.c_uint32 * (GW_MAX_ENC + 1)),
+        ("stacked_attacks", C.c_int32),
+        ("observe_self", C.c_int32),
+        ("no_overlap_at_reset", C.c_int32),
+        ("state_order", C.c_int32),
+        ("done_kind", C.c_uint32),
+        ("obs_range", C.c_int32),
+        ("target_agent", C.c_int32),
+        ("nav_agent", C.c_int32),
+        ("agents", C.POINTER(AgentSpec)),
+    ]
+
+
+class CompiledConfig:
+    """Owns a ``Config`` and the ``AgentSpec`` array it points to."""
+
+    def __init__(self, rows, cols, specs, sim_kind, overlap, attack_mapping,
+                 stacked_attacks=False, observe_self=True, no_overlap_at_reset=False,
+                 state_order=GW_ORDER_POSITION_HEALTH, done_kind=GW_DONE_ACTIVE,
+                 obs_range=0, target_agent=-1, nav_agent=-1):
+        self.n_agents = len(specs)
+        self._specs = (AgentSpec * max(1, self.n_agents))()
+        for i, s in enumerate(specs):
+            self._specs[i] = s
+        cfg = Config()
+        cfg.rows, cfg.cols, cfg.n_agents, cfg.sim_kind = rows, cols, self.n_agents, sim_kind
+        for e in range(GW_MAX_ENC + 1):
+            cfg.overlap[e] = int(overlap.get(e, 0))
+            cfg.attack_mapping[e] = int(attack_mapping.get(e, 0))
+        cfg.stacked_attacks = int(bool(stacked_attacks))
+        cfg.observe_self = int(bool(observe_self))
+        cfg.no_overlap_at_reset = int(bool(no_overlap_at_reset))
+        cfg.state_order = state_order
+        cfg.done_kind = done_kind
+        cfg.obs_range = obs_range
+        cfg.target_agent = target_agent
+        cfg.nav_agent = nav_agent
+        cfg.agents = C.cast(self._specs, C.POINTER(AgentSpec))
+        self.cfg = cfg
+        self.rows, self.cols = rows, cols
+        self.obs_side = 2 * obs_range + 1
+        self.specs = list(specs)
+
+    def ptr(self):
+        return C.byref(self.cfg)

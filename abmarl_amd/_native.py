@@ -1,0 +1,77 @@
+"""Loader for the HIP engine library (libgw_engine.so, built in-tree).
+
+The product path has no CPU fallback: if the library or a GPU is missing,
+``lib()`` raises.
+"""
+import ctypes as C
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(PKG, 'csrc', 'gw_engine.hip')
+INCLUDE = os.path.join(os.path.dirname(PKG), 'include', 'gw_engine.h')
+LIB = os.path.join(PKG, '_build', 'libgw_engine.so')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = os.environ.get('GW_OFFLOAD_ARCH', 'gfx950')
+
+# every entry point declared in include/gw_engine.h: (restype, argtypes)
+_vp, _i32, _u32, _u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+SIGNATURES = {
+    'gw_create': (_i32, [_vp, _i32, _i32, C.POINTER(_vp)]),
+    'gw_seed': (_i32, [_vp, _vp, _vp]),
+    'gw_reset': (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_set_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_random_actions': (_i32, [_vp, _u64, _u32, _vp, _vp]),
+    'gw_destroy': (_i32, [_vp]),
+    'gw_num_envs': (_i32, [_vp]),
+    'gw_obs_side': (_i32, [_vp]),
+    'gw_last_error': (C.c_char_p, []),
+    'gw_abi_version': (_i32, []),
+}
+
+
+def build(force=False, verbose=False):
+    """Compile the engine for gfx950 with hipcc (works without a GPU)."""
+    deps = [SRC, INCLUDE]
+    if not force and os.path.exists(LIB) and \
+            os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off',
+           '-fPIC', '-shared', '-Wno-unused-result', '-o', LIB + '.tmp', SRC]
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(LIB + '.tmp', LIB)
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    """The loaded engine library; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"HIP engine library {LIB} is missing; run "
+                               "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().gw_last_error().decode(errors='replace')
+        raise EngineError(f"{what} failed with status {status}: {msg}")

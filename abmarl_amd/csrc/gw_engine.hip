@@ -1,0 +1,1071 @@
+// gw_engine.hip — MI355X (gfx950) batched GridWorld step engine.
+//
+// Execution model: ONE WAVEFRONT PER ENVIRONMENT, one lane per entity
+// (A <= 64).  The reference's step is a sequence of Python loops over the
+// agents dict whose random draws come from one sequential MT19937 stream
+// (numpy legacy RandomState); everything that changes the RNG stream or the
+// grid in reference order is kept in reference order here, and everything
+// else is lane-parallel:
+//
+//   attack pass (team_battle_example.py:35-47 / actor.py:306-501)
+//       serial over attackers; each attacker's window scan is one ballot,
+//       candidates are extracted in (window cell, in-cell insertion order)
+//       with a wave min-reduction, accuracy draws / permutation draws are
+//       issued in reference order from a register-cached MT19937 block.
+//   move pass   (team_battle_example.py:50-55 / actor.py:82-114)
+//       serial over movers; Grid.query is one ballot over the lanes.
+//   observation (all_step_manager.py:68-71 / observer.py:204-250)
+//       lane-parallel window gather from an LDS occupancy table
+//       (count | xor-of-encodings per cell, rebuilt after the moves); the
+//       rare cells with >= 2 candidate occupants (np.random.choice draws) are
+//       resolved afterwards in (agent, row, col) order.
+//   reward / done / __all__ (smart.py:101-117, done.py:39-56,140-153,
+//       all_step_manager.py:72-93): lane-parallel + ballots.
+//
+// The grid's insertion-ordered dict cells are represented by a per-agent
+// placement sequence number (seq): the order of agents inside a cell is the
+// order of their seq.  No grid array lives in HBM.
+//
+// Data layout in HBM (SoA, env-major, lane-contiguous => coalesced):
+//   pos[E][A] int2, health[E][A] f64, flags[E][A] u8, seq[E][A] u32,
+//   mt[E][640] u32 (key[624], pos @624, seq counter @625), steps[E] i32.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include "../../include/gw_engine.h"
+
+#define WAVE 64
+#define F_IN_GRID 1u
+#define F_LIVE 2u
+#define F_ACTIVE 4u
+#define MT_POS_SLOT 624
+#define MT_CTR_SLOT 625
+#define SEQ_RENORM (1u << 23)
+
+namespace {
+
+// ------------------------------------------------------------ device config
+struct DevAgent {               // per-entity constants (spec table in HBM)
+    int32_t enc;
+    uint32_t kind;
+    int32_t init_r, init_c;
+    int32_t view_range, move_range, attack_range, simul;
+    double strength, accuracy, init_health;
+};
+
+struct Params {
+    // engine state
+    int2* pos; double* health; uint8_t* flags; uint32_t* seq; uint32_t* mt; int32_t* steps;
+    const DevAgent* spec;
+    // I/O
+    const int32_t* actions; int32_t* obs; double* reward; uint8_t* done; uint8_t* all_done;
+    uint64_t* acting; uint32_t* err;
+    const uint8_t* mask; const uint8_t* prev_all_done; int32_t horizon;
+    // config
+    int32_t E, A, H, W, max_enc, sim_kind, nav, target;
+    int32_t observe_self, stacked, no_overlap_at_reset, state_order;
+    uint32_t done_kind;
+    uint32_t overlap[GW_MAX_ENC + 1];
+    uint32_t amap[GW_MAX_ENC + 1];
+};
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ void wave_sync()
+{
+    // one wavefront per env: LDS ops of a wave complete in order; this keeps
+    // the compiler from moving LDS accesses across cross-lane hand-offs.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int32_t rl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+__device__ __forceinline__ double rld(double v, int l)
+{
+    uint64_t b = __double_as_longlong(v);
+    uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
+    uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, WAVE));
+    return uni(v);
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, WAVE);
+    return uni(v);
+}
+
+__device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
+
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const int l = lane_id();
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        uint32_t t = (uint32_t)__shfl_up((int)v, off, WAVE);
+        if (l >= off) v += t;
+    }
+    return v;
+}
+
+// ------------------------------------------------------------ MT19937
+// numpy legacy RandomState (mt19937.c): key[] lives in LDS; tempered output
+// words are cached one per lane (a 64-word block), so a draw is one
+// v_readlane; the twist is lane-parallel in chunks of 64 (every write's
+// dependency i-227 is >= 3 chunks back; i+1 is read before any lane writes).
+struct Rng {
+    uint32_t* key;      // LDS [624]
+    uint32_t cache;     // tempered key[base + lane]
+    int pos;            // next index (wave-uniform)
+    int base;           // cached block base (wave-uniform), -1 = none
+    bool dirty;         // twisted since load
+
+    __device__ __forceinline__ void twist()
+    {
+        const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
+        const int l = lane_id();
+        wave_sync();
+        for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
+            int i = b + l;
+            uint32_t nv = 0;
+            if (i < GW_MT_N - 1) {
+                uint32_t y = (key[i] & UP) | (key[i + 1] & LO);
+                int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
+                nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+            }
+            wave_sync();
+            if (i < GW_MT_N - 1) key[i] = nv;
+            wave_sync();
+        }
+        {
+            uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
+            uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+            wave_sync();
+            if (l == 0) key[GW_MT_N - 1] = nv;
+            wave_sync();
+        }
+        pos = 0;
+        base = -1;
+        dirty = true;
+    }
+
+    __device__ __forceinline__ uint32_t next()
+    {
+        if (pos == GW_MT_N) twist();
+        int b = pos & ~(WAVE - 1);
+        if (b != base) {
+            int i = b + lane_id();
+            uint32_t y = i < GW_MT_N ? key[i] : 0u;
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= (y >> 18);
+            cache = y;
+            base = b;
+        }
+        uint32_t v = rl(cache, pos & (WAVE - 1));
+        pos = pos + 1;
+        return v;
+    }
+
+    // np.random.uniform(): 53-bit double from two words
+    __device__ __forceinline__ double uniform()
+    {
+        uint32_t a = next() >> 5;
+        uint32_t b = next() >> 6;
+        return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    }
+
+    // masked rejection draw on [0, max]; zero draws when max == 0
+    __device__ __forceinline__ uint32_t interval(uint32_t max)
+    {
+        if (max == 0) return 0;
+        uint32_t m = max;
+        m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+        uint32_t v;
+        do { v = next() & m; } while (v > max);
+        return v;
+    }
+};
+
+// ------------------------------------------------------------ per-env context
+struct Lane {
+    // constants
+    int enc; uint32_t kind; int view, mrange, arange, simul;
+    double strength, accuracy, init_health;
+    uint32_t ov;      // overlap mask of this lane's encoding
+    int init_r, init_c;
+    // state
+    int r, c; uint32_t seq; double health; bool in_grid, live, active;
+    double reward;
+};
+
+__device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool valid)
+{
+    const int l = lane_id();
+    if (valid) {
+        const DevAgent s = p.spec[l];
+        L.enc = s.enc; L.kind = s.kind; L.view = s.view_range; L.mrange = s.move_range;
+        L.arange = s.attack_range; L.simul = s.simul; L.strength = s.strength;
+        L.accuracy = s.accuracy; L.init_health = s.init_health; L.init_r = s.init_r;
+        L.init_c = s.init_c;
+        L.ov = p.overlap[s.enc];
+        size_t k = (size_t)e * p.A + l;
+        int2 q = p.pos[k];
+        L.r = q.x; L.c = q.y;
+        L.seq = p.seq[k];
+        L.health = p.health[k];
+        uint8_t f = p.flags[k];
+        L.in_grid = f & F_IN_GRID; L.live = f & F_LIVE; L.active = f & F_ACTIVE;
+    } else {
+        L.enc = 0; L.kind = 0; L.view = L.mrange = L.arange = L.simul = 0;
+        L.strength = L.accuracy = L.init_health = 0; L.init_r = L.init_c = -1; L.ov = 0;
+        L.r = L.c = -1000; L.seq = 0; L.health = 0; L.in_grid = L.live = L.active = false;
+    }
+    L.reward = 0.0;
+}
+
+__device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L, bool valid)
+{
+    if (!valid) return;
+    size_t k = (size_t)e * p.A + lane_id();
+    p.pos[k] = make_int2(L.r, L.c);
+    p.seq[k] = L.seq;
+    p.health[k] = L.health;
+    p.flags[k] = (uint8_t)((L.in_grid ? F_IN_GRID : 0) | (L.live ? F_LIVE : 0) | (L.active ? F_ACTIVE : 0));
+}
+
+// LDS carve-up per wave (dynamic shared memory, 16-B aligned pieces)
+struct Smem {
+    uint32_t* key;     // [624]  (pad 640)
+    uint32_t* cell;    // [HW]   count | xor(enc) << 16
+    int8_t* stage;     // [A*SS] observation staging (pad to 16)
+    uint64_t* avail;   // [(max_enc+1) * 64] reset availability bitmaps
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, bool reset)
+{
+    size_t b = align16(GW_MT_STRIDE * 4) + align16((size_t)HW * 4) + align16((size_t)A * SS);
+    if (reset) b += align16((size_t)(max_enc + 1) * 64 * 8);
+    return b;
+}
+
+__device__ __forceinline__ Smem carve(char* base, int HW, int A, int SS)
+{
+    Smem s;
+    s.key = (uint32_t*)base; base += align16(GW_MT_STRIDE * 4);
+    s.cell = (uint32_t*)base; base += align16((size_t)HW * 4);
+    s.stage = (int8_t*)base; base += align16((size_t)A * SS);
+    s.avail = (uint64_t*)base;
+    return s;
+}
+
+__device__ __forceinline__ void load_rng(const Params& p, int e, Smem& sm, Rng& rng)
+{
+    const uint32_t* src = p.mt + (size_t)e * GW_MT_STRIDE;
+    const int l = lane_id();
+    for (int i = l; i < GW_MT_STRIDE / 4; i += WAVE)
+        ((uint4*)sm.key)[i] = ((const uint4*)src)[i];
+    wave_sync();
+    rng.key = sm.key;
+    rng.pos = uni((int32_t)sm.key[MT_POS_SLOT]);
+    rng.base = -1;
+    rng.cache = 0;
+    rng.dirty = false;
+}
+
+__device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, const Rng& rng, uint32_t ctr)
+{
+    uint32_t* dst = p.mt + (size_t)e * GW_MT_STRIDE;
+    const int l = lane_id();
+    if (rng.dirty) {
+        wave_sync();
+        for (int i = l; i < GW_MT_N / 4; i += WAVE) ((uint4*)dst)[i] = ((const uint4*)sm.key)[i];
+    }
+    if (l == 0) { dst[MT_POS_SLOT] = (uint32_t)rng.pos; dst[MT_CTR_SLOT] = ctr; }
+}
+
+// rebuild the LDS occupancy table from the lanes (count | xor enc << 16)
+__device__ __forceinline__ void build_cells(const Params& p, Smem& sm, const Lane& L)
+{
+    const int HW = p.H * p.W;
+    for (int i = lane_id(); i < HW; i += WAVE) sm.cell[i] = 0u;
+    wave_sync();
+    if (L.in_grid) {
+        int ci = L.r * p.W + L.c;
+        atomicAdd(&sm.cell[ci], 1u);
+        atomicXor(&sm.cell[ci], (uint32_t)L.enc << 16);
+    }
+    wave_sync();
+}
+
+// ------------------------------------------------------------ observation
+// PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
+template <int S>
+__device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L)
+{
+    constexpr int SS = S * S;
+    constexpr int R = S / 2;
+    constexpr int NW = (SS + 63) / 64;
+    const int l = lane_id();
+    const int A = p.A;
+    const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
+    uint64_t ev[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) ev[w] = 0;
+
+    if (l < A) {
+        int8_t* st = sm.stage + l * SS;
+        for (int wr = 0; wr < S; wr++) {
+            const int gr = L.r - R + wr;
+            for (int wc = 0; wc < S; wc++) {
+                const int gc = L.c - R + wc;
+                const int k = wr * S + wc;
+                int v = -2;
+                if (obs_me) {
+                    if (gr < 0 || gr >= p.H || gc < 0 || gc >= p.W) v = -1;
+                    else {
+                        uint32_t w = sm.cell[gr * p.W + gc];
+                        int cnt = (int)(w & 0xffffu);
+                        int x = (int)(w >> 16);
+                        if (!p.observe_self && L.in_grid && gr == L.r && gc == L.c) { cnt -= 1; x ^= L.enc; }
+                        if (cnt == 0) v = 0;
+                        else if (cnt == 1) v = x;
+                        else { v = 0; ev[k >> 6] |= 1ull << (k & 63); }
+                    }
+                }
+                st[k] = (int8_t)v;
+            }
+        }
+    }
+    wave_sync();
+
+    // serial: cells with >= 2 candidates draw np.random.choice in
+    // (agent, row, col) order (observer.py:224-246)
+    uint64_t any = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) any |= ev[w];
+    uint64_t olanes = __ballot(any != 0);
+    while (olanes) {
+        const int o = first_lane(olanes);
+        olanes &= olanes - 1;
+        const int orr = rl(L.r, o), oc = rl(L.c, o);
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            uint32_t lo = rl((uint32_t)ev[w], o), hi = rl((uint32_t)(ev[w] >> 32), o);
+            uint64_t bits = ((uint64_t)hi << 32) | lo;
+            while (bits) {
+                const int k = w * 64 + (int)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const int gr = orr - R + k / S, gc = oc - R + k % S;
+                const bool mem = l < A && L.in_grid && L.r == gr && L.c == gc && (p.observe_self || l != o);
+                uint64_t mm = __ballot(mem);
+                const int n = __popcll(mm);
+                const uint32_t j = rng.interval((uint32_t)(n - 1));
+                // the j-th member in insertion (seq) order
+                uint32_t sel = 0;
+                for (uint32_t t = 0; t <= j; t++) {
+                    uint32_t key = (mem && ((mm >> l) & 1)) ? L.seq : 0xffffffffu;
+                    uint32_t mn = wave_min(key);
+                    uint64_t hit = __ballot(((mm >> l) & 1) && L.seq == mn);
+                    sel = first_lane(hit);
+                    mm &= ~(1ull << sel);
+                }
+                const int val = rl(L.enc, (int)sel);
+                if (l == 0) sm.stage[o * SS + k] = (int8_t)val;
+            }
+        }
+    }
+    wave_sync();
+
+    // stage (int8) -> obs (int32), 4 values per lane per iteration, coalesced
+    const int total = A * SS;                  // multiple of 4? handle tail
+    int32_t* out = p.obs + (size_t)e * total;
+    for (int i = l * 4; i < total; i += WAVE * 4) {
+        if (i + 3 < total && (((size_t)e * total + i) & 3) == 0) {
+            uint32_t w = *(const uint32_t*)(sm.stage + i);
+            int4 v = make_int4((int8_t)(w & 0xff), (int8_t)((w >> 8) & 0xff),
+                               (int8_t)((w >> 16) & 0xff), (int8_t)(w >> 24));
+            *(int4*)(out + i) = v;
+        } else {
+            for (int q = i; q < i + 4 && q < total; q++) out[q] = sm.stage[q];
+        }
+    }
+}
+
+// ------------------------------------------------------------ attack
+// BinaryAttackActor.process_action for attacker a with k attacks.
+// Returns status (attempted) and appends the attacked lanes (in list order)
+// to `list` (registers of lane t hold list[t]).  Applies damage.
+__device__ __forceinline__ bool attack_one(const Params& p, Rng& rng, Lane& L, int a, int k,
+                                           int& nlist, int& list)
+{
+    const int l = lane_id();
+    nlist = 0;
+    const uint32_t akind = rl(L.kind, a);
+    if (!(akind & GW_K_ATTACKING)) return false;
+    if (k == 0) return false;
+    const int ar = rl(L.r, a), ac = rl(L.c, a), aenc = rl(L.enc, a);
+    const int R = rl(L.arange, a);
+    const double acc = rld(L.accuracy, a);
+    const uint32_t amap = p.amap[aenc];
+    const int D = 2 * R + 1;
+    const int dr = L.r - ar, dc = L.c - ac;
+    const bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
+                      dr >= -R && dr <= R && dc >= -R && dc <= R;
+    const uint32_t ckey = cand ? ((uint32_t)((dr + R) * D + (dc + R)) << 24) | L.seq : 0xffffffffu;
+    uint64_t cm = __ballot(cand);
+    int rank = -1;
+    int n = 0;
+    while (cm) {
+        int j;
+        if ((cm & (cm - 1)) == 0) j = first_lane(cm);
+        else {
+            uint32_t mn = wave_min(((cm >> l) & 1) ? ckey : 0xffffffffu);
+            j = first_lane(__ballot(((cm >> l) & 1) && ckey == mn));
+        }
+        cm &= ~(1ull << j);
+        const double u = rng.uniform();                     // _basic_criteria draw
+        if (u > acc) continue;
+        if (l == j) rank = n;
+        n++;
+    }
+    if (n == 0) return true;                                // (True, [])
+    // _subset_attackables: list[t] (lane t) = accepted rank
+    int pick = -1;
+    if (!p.stacked && k > n) {
+        pick = l < n ? l : -1;
+        nlist = n;
+    } else if (p.stacked) {
+        for (int t = 0; t < k; t++) {
+            int idx = (int)rng.interval((uint32_t)(n - 1));
+            if (l == t) pick = idx;
+        }
+        nlist = k;
+    } else {
+        int perm = l;                                       // permutation(n)[:k]
+        for (int i = n - 1; i >= 1; i--) {
+            int j = (int)rng.interval((uint32_t)i);
+            int pi = rl(perm, i), pj = rl(perm, j);
+            if (l == i) perm = pj;
+            if (l == j) perm = pi;
+        }
+        pick = l < k ? perm : -1;
+        nlist = k;
+    }
+    // translate ranks to lanes
+    list = -1;
+    for (int t = 0; t < nlist; t++) {
+        const int pr = rl(pick, t);
+        const int lane_t = first_lane(__ballot(rank == pr));
+        if (l == t) list = lane_t;
+    }
+    // apply damage in list order (actor.py:353-358)
+    const double strength = rld(L.strength, a);
+    for (int t = 0; t < nlist; t++) {
+        const int b = rl(list, t);
+        if (l == b && L.active) {
+            double h = L.health - strength;
+            if (0.0 > h) h = 0.0;
+            if (1.0 < h) h = 1.0;
+            L.health = h;
+            L.active = h > 0.0;
+            if (!L.active) L.in_grid = false;               // grid.remove
+        }
+    }
+    return true;
+}
+
+// MoveActor.process_action
+__device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr, int mc, uint32_t& ctr)
+{
+    const int l = lane_id();
+    const uint32_t akind = rl(L.kind, a);
+    if (!(akind & GW_K_MOVING)) return false;               // returns None
+    const int ar = rl(L.r, a), ac = rl(L.c, a);
+    const int nr = ar + mr, nc = ac + mc;
+    if (!(0 <= nr && nr < p.H && 0 <= nc && nc < p.W)) return false;
+    if (nr == ar && nc == ac) return true;
+    const uint32_t aov = rl(L.ov, a);
+    const bool blocks = l < p.A && L.in_grid && L.r == nr && L.c == nc && !((aov >> L.enc) & 1u);
+    if (__ballot(blocks)) return false;                     // Grid.query
+    if (l == a) { L.r = nr; L.c = nc; L.seq = ctr; }        // remove + place (appended)
+    ctr++;
+    return true;
+}
+
+__device__ __forceinline__ void renorm_seq(const Params& p, Lane& L, uint32_t& ctr)
+{
+    // keep seq < 2^24 (attack keys use 24 bits): rank-compress, order preserved
+    const int l = lane_id();
+    uint32_t rank = 0;
+    for (int i = 0; i < p.A; i++) {
+        uint32_t si = rl(L.seq, i);
+        bool gi = __builtin_amdgcn_readlane((int)L.in_grid, i);
+        if (gi && si < L.seq) rank++;
+    }
+    if (l < p.A && L.in_grid) L.seq = rank;
+    ctr = (uint32_t)__popcll(__ballot(l < p.A && L.in_grid));
+}
+
+// ------------------------------------------------------------ kernels
+template <int S>
+__global__ __launch_bounds__(WAVE) void step_kernel(Params p)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int e = blockIdx.x;
+    if (e >= p.E) return;
+    constexpr int SS = S * S;
+    const int l = lane_id();
+    const int A = p.A;
+    const bool valid = l < A;
+    Smem sm = carve(smem_raw, p.H * p.W, A, SS);
+    Lane L;
+    load_lane(p, e, L, valid);
+    Rng rng;
+    load_rng(p, e, sm, rng);
+    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
+    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
+
+    // actions (lane = agent); attack == -1 marks "not in action_dict"
+    int mr = 0, mc = 0, ak = -1;
+    if (valid) {
+        const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
+        mr = ap[0]; mc = ap[1]; ak = ap[2];
+    }
+    const bool acting = valid && L.live && ak >= 0;
+    const uint64_t act_mask = __ballot(acting);
+
+    if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
+        // attack pass (team_battle_example.py:35-47)
+        // the active check is re-evaluated per attacker: earlier attacks can kill
+        for (uint64_t it = act_mask; it; it &= it - 1) {
+            const int a = first_lane(it);
+            if (!rl((int)L.active, a)) continue;
+            int nlist, list;
+            const bool status = attack_one(p, rng, L, a, rl(ak, a), nlist, list);
+            if (status) {
+                if (nlist == 0) { if (l == a) L.reward -= 0.1; }
+                else {
+                    for (int t = 0; t < nlist; t++) {
+                        const int b = rl(list, t);
+                        const bool dead = !rl((int)L.active, b);
+                        if (dead) {
+                            if (l == b) L.reward -= 1.0;
+                            if (l == a) L.reward += 1.0;
+                        }
+                    }
+                }
+            }
+        }
+        // move pass (:50-55)
+        for (uint64_t it = act_mask; it; it &= it - 1) {
+            const int a = first_lane(it);
+            if (!rl((int)L.active, a)) continue;
+            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr);
+            if (!ok && l == a) L.reward -= 0.1;
+        }
+        // entropy (:58-59)
+        if (acting) L.reward -= 0.01;
+    } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        const int n = p.nav, t = p.target;
+        if ((act_mask >> n) & 1) {
+            const bool ok = move_one(p, L, n, rl(mr, n), rl(mc, n), ctr);
+            if (!ok && l == n) L.reward -= 0.1;
+            const bool at = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+            if (at && l == n) L.reward += 1.0;
+            if (l == n) L.reward -= 0.01;
+        }
+    }
+
+    // observations of the live agents (all_step_manager.py:68-71)
+    build_cells(p, sm, L);
+    observe_all<S>(p, e, sm, rng, L);
+
+    // rewards, dones (:72-79, smart.py:101-111)
+    bool dn;
+    if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        const int n = p.nav, t = p.target;
+        dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+    } else {
+        dn = !L.active;
+    }
+    if (valid) {
+        size_t k = (size_t)e * A + l;
+        p.reward[k] = L.live ? L.reward : 0.0;
+        p.done[k] = L.live ? (uint8_t)dn : (uint8_t)1;
+    }
+    const bool live_after = valid && L.live && !dn;
+    // get_all_done (done.py:49-56,147-153) or maze target reached
+    bool all;
+    if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        all = dn;
+    } else {
+        all = true;
+        if (p.done_kind & GW_DONE_ACTIVE) all = all && (__ballot(valid && L.active) == 0);
+        if (p.done_kind & GW_DONE_ONE_TEAM) {
+            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u);
+            all = all && (__popc(bits) <= 1);
+        }
+    }
+    const bool any_left = __ballot(live_after) != 0;
+    L.live = live_after;
+    if (l == 0) {
+        p.all_done[e] = (uint8_t)(all || !any_left);
+        p.steps[e] += 1;
+        if (p.acting) p.acting[e] += (uint64_t)__popcll(act_mask);
+    }
+    store_lane(p, e, L, valid);
+    store_rng(p, e, sm, rng, ctr);
+}
+
+template <int S>
+__global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int e = blockIdx.x;
+    if (e >= p.E) return;
+    // reset everything when no selector is given; otherwise the union of the
+    // explicit mask, the previous step's __all__ and the horizon
+    bool go;
+    if (p.mask == nullptr && p.prev_all_done == nullptr && p.horizon <= 0) go = true;
+    else go = (p.mask && p.mask[e]) || (p.prev_all_done && p.prev_all_done[e]) ||
+              (p.horizon > 0 && p.steps[e] >= p.horizon);
+    if (!go) return;
+
+    constexpr int SS = S * S;
+    const int l = lane_id();
+    const int A = p.A;
+    const bool valid = l < A;
+    const int HW = p.H * p.W;
+    Smem sm = carve(smem_raw, HW, A, SS);
+    Lane L;
+    load_lane(p, e, L, valid);
+    Rng rng;
+    load_rng(p, e, sm, rng);
+    uint32_t ctr = 0;
+    uint32_t err = 0;
+
+    // AllStepManager.reset: done_agents = non-Agent entities
+    L.live = valid && (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
+    L.in_grid = false;
+    L.reward = 0.0;
+    const bool has_health = __ballot(valid && (L.kind & GW_K_HEALTH)) != 0;
+
+    auto health_reset = [&]() {
+        // state.py:629-641, agent order, one uniform() per random health
+        for (int a = 0; a < A; a++) {
+            const uint32_t k = rl(L.kind, a);
+            if (!(k & GW_K_HEALTH)) continue;
+            const double ih = rld(L.init_health, a);
+            double h = ih >= 0.0 ? ih : rng.uniform();
+            if (0.0 > h) h = 0.0;
+            if (1.0 < h) h = 1.0;
+            if (l == a) { L.health = h; L.active = h > 0.0; }
+        }
+    };
+
+    auto position_reset = [&]() -> bool {
+        // state.py:88-166 — availability lists are bitmaps (the reference's
+        // lists stay in ascending cell order under list.remove)
+        const int nwords = (HW + 63) / 64;
+        for (int enc = 1; enc <= p.max_enc; enc++) {
+            uint64_t w = 0;
+            if (l < nwords) {
+                int rem = HW - l * 64;
+                w = rem >= 64 ? ~0ull : ((1ull << rem) - 1);
+            }
+            sm.avail[enc * 64 + l] = w;
+        }
+        wave_sync();
+        for (int pass = 0; pass < 2; pass++) {
+            for (int a = 0; a < A; a++) {
+                const int ir = rl(L.init_r, a), ic = rl(L.init_c, a);
+                const bool has_ip = ir >= 0;
+                if ((pass == 0) != has_ip) continue;
+                const int aenc = rl(L.enc, a);
+                int r, c;
+                if (has_ip) { r = ir; c = ic; }
+                else {
+                    const uint64_t w = (l < nwords) ? sm.avail[aenc * 64 + l] : 0ull;
+                    const uint32_t pc = (l < nwords) ? (uint32_t)__popcll(w) : 0u;
+                    const uint32_t incl = wave_incl_scan(pc);
+                    const uint32_t total = rl(incl, WAVE - 1);
+                    if (total == 0) { err |= GW_ERR_NO_CELL; return false; }
+                    const uint32_t idx = rng.interval(total - 1);
+                    const uint32_t excl = incl - pc;
+                    const bool mine = l < nwords && excl <= idx && idx < incl;
+                    int cell = 0;
+                    if (mine) {
+                        uint64_t ww = w;
+                        for (uint32_t t = excl; t < idx; t++) ww &= ww - 1;
+                        cell = l * 64 + (int)__builtin_ctzll(ww);
+                    }
+                    cell = rl(cell, first_lane(__ballot(mine)));
+                    r = cell / p.W; c = cell % p.W;
+                }
+                // Grid.place -> query (grid.py:81-129)
+                const uint32_t aov = rl(L.ov, a);
+                const bool blocks = valid && L.in_grid && L.r == r && L.c == c && !((aov >> L.enc) & 1u);
+                if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
+                if (l == a) { L.r = r; L.c = c; L.in_grid = true; L.seq = ctr; }
+                ctr++;
+                // _update_available_positions (state.py:126-141)
+                const int cell = r * p.W + c;
+                if (l == (cell >> 6)) {
+                    for (int enc = 1; enc <= p.max_enc; enc++)
+                        if (p.no_overlap_at_reset || !((aov >> enc) & 1u))
+                            sm.avail[enc * 64 + l] &= ~(1ull << (cell & 63));
+                }
+                wave_sync();
+            }
+        }
+        return true;
+    };
+
+    bool ok;
+    if (p.state_order == GW_ORDER_POSITION_HEALTH) {
+        ok = position_reset();
+        if (ok && has_health) health_reset();
+    } else {
+        if (has_health) health_reset();
+        ok = position_reset();
+    }
+    // agents without HealthAgent keep active = True
+    if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;
+
+    if (ok) {
+        build_cells(p, sm, L);
+        observe_all<S>(p, e, sm, rng, L);
+    } else {
+        int32_t* out = p.obs + (size_t)e * A * SS;
+        for (int i = l; i < A * SS; i += WAVE) out[i] = -2;
+    }
+    if (l == 0) {
+        p.steps[e] = 0;
+        if (p.err) p.err[e] |= err;
+    }
+    store_lane(p, e, L, valid);
+    store_rng(p, e, sm, rng, ctr);
+}
+
+__global__ void seed_kernel(uint32_t* mt, const uint32_t* seeds, int E)
+{
+    // np.random.seed(int) == init_genrand; one thread per env (once per run)
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    uint32_t* k = mt + (size_t)e * GW_MT_STRIDE;
+    uint32_t s = seeds[e];
+    for (int i = 0; i < GW_MT_N; i++) {
+        k[i] = s;
+        s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(i + 1);
+    }
+    k[MT_POS_SLOT] = GW_MT_N;
+    k[MT_CTR_SLOT] = 0;
+}
+
+// Philox-4x32-10
+__device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
+{
+    for (int i = 0; i < 10; i++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * ctr.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr.z;
+        ctr = make_uint4((uint32_t)(p1 >> 32) ^ ctr.y ^ key.x, (uint32_t)p1,
+                         (uint32_t)(p0 >> 32) ^ ctr.w ^ key.y, (uint32_t)p0);
+        key.x += 0x9E3779B9u;
+        key.y += 0xBB67AE85u;
+    }
+    return ctr;
+}
+
+__global__ void random_actions_kernel(const DevAgent* spec, int E, int A, uint64_t key,
+                                      uint32_t step, int32_t* actions)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E * A) return;
+    const int e = i / A, a = i % A;
+    const DevAgent s = spec[a];
+    uint4 r = philox(make_uint4((uint32_t)e, step, (uint32_t)a, 0x5EED),
+                     make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
+    const int m = s.move_range;
+    const uint32_t span = (uint32_t)(2 * m + 1);
+    int32_t* o = actions + (size_t)i * GW_ACT_DIM;
+    o[0] = (s.kind & GW_K_MOVING) ? (int32_t)(r.x % span) - m : 0;
+    o[1] = (s.kind & GW_K_MOVING) ? (int32_t)(r.y % span) - m : 0;
+    o[2] = (s.kind & GW_K_ATTACKING) ? (int32_t)(r.z % (uint32_t)(s.simul + 1)) : 0;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+struct gw_engine {
+    int device;
+    int E, A, H, W, S, max_enc;
+    Params base;
+    DevAgent* d_spec;
+    size_t smem_step, smem_reset;
+};
+
+static thread_local char g_err[512];
+
+static void set_err(const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+#define HIPCHK(x)                                                                 \
+    do {                                                                          \
+        hipError_t _e = (x);                                                      \
+        if (_e != hipSuccess) {                                                   \
+            set_err("%s: %s", #x, hipGetErrorString(_e));                        \
+            return GW_E_HIP;                                                      \
+        }                                                                         \
+    } while (0)
+
+template <int S>
+static hipError_t launch_step(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(step_kernel<S>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    return hipGetLastError();
+}
+
+template <int S>
+static hipError_t launch_reset(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(reset_kernel<S>, dim3(g->E), dim3(WAVE), g->smem_reset, st, p);
+    return hipGetLastError();
+}
+
+#define DISPATCH_S(S_, FN, ...)                      \
+    switch (S_) {                                    \
+    case 1: return FN<1>(__VA_ARGS__);               \
+    case 3: return FN<3>(__VA_ARGS__);               \
+    case 5: return FN<5>(__VA_ARGS__);               \
+    case 7: return FN<7>(__VA_ARGS__);               \
+    case 9: return FN<9>(__VA_ARGS__);               \
+    case 11: return FN<11>(__VA_ARGS__);             \
+    case 13: return FN<13>(__VA_ARGS__);             \
+    case 15: return FN<15>(__VA_ARGS__);             \
+    default: return hipErrorInvalidValue;            \
+    }
+
+static hipError_t do_step(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    DISPATCH_S(g->S, launch_step, g, p, st);
+}
+
+static hipError_t do_reset(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    DISPATCH_S(g->S, launch_reset, g, p, st);
+}
+
+template <int S>
+static hipError_t set_smem_attr(size_t step_b, size_t reset_b)
+{
+    hipError_t e = hipFuncSetAttribute((const void*)step_kernel<S>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)step_b);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)reset_kernel<S>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)reset_b);
+}
+
+static hipError_t set_attrs(int S, size_t a, size_t b)
+{
+    DISPATCH_S(S, set_smem_attr, a, b);
+}
+
+extern "C" {
+
+int32_t gw_abi_version(void) { return 1; }
+const char* gw_last_error(void) { return g_err; }
+
+gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
+{
+    if (!cfg || !out || n_envs <= 0) { set_err("invalid argument"); return GW_E_INVALID; }
+    const int A = cfg->n_agents, HW = cfg->rows * cfg->cols;
+    if (A <= 0 || A > GW_MAX_AGENTS) {
+        set_err("n_agents=%d outside 1..%d (one wavefront lane per entity)", A, GW_MAX_AGENTS);
+        return GW_E_UNSUPPORTED;
+    }
+    if (cfg->rows <= 0 || cfg->cols <= 0 || HW > GW_MAX_CELLS) {
+        set_err("grid %dx%d outside the engine's %d cells", cfg->rows, cfg->cols, GW_MAX_CELLS);
+        return GW_E_UNSUPPORTED;
+    }
+    if (cfg->obs_range < 0 || cfg->obs_range > GW_MAX_RANGE) {
+        set_err("obs_range %d > %d", cfg->obs_range, GW_MAX_RANGE);
+        return GW_E_UNSUPPORTED;
+    }
+    if (cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_MAZE_NAV) {
+        set_err("unknown sim_kind %d", cfg->sim_kind);
+        return GW_E_INVALID;
+    }
+    int max_enc = 0;
+    for (int a = 0; a < A; a++) {
+        const gw_agent_spec& s = cfg->agents[a];
+        if (s.encoding < 1 || s.encoding > GW_MAX_ENC) { set_err("agent %d encoding %d", a, s.encoding); return GW_E_UNSUPPORTED; }
+        if (s.kind & GW_K_BLOCKING) { set_err("blocking agents are not built yet"); return GW_E_UNSUPPORTED; }
+        if ((s.kind & GW_K_GRID_OBSERVER) && s.view_range != cfg->obs_range) {
+            set_err("agent %d view_range %d != obs_range %d", a, s.view_range, cfg->obs_range);
+            return GW_E_UNSUPPORTED;
+        }
+        if ((s.kind & GW_K_ATTACKING) && s.attack_range > GW_MAX_RANGE) { set_err("attack_range"); return GW_E_UNSUPPORTED; }
+        if (s.init_row >= cfg->rows || s.init_col >= cfg->cols) { set_err("agent %d initial position outside the grid", a); return GW_E_INVALID; }
+        if (s.encoding > max_enc) max_enc = s.encoding;
+    }
+    if (cfg->sim_kind == GW_SIM_MAZE_NAV &&
+        (cfg->nav_agent < 0 || cfg->nav_agent >= A || cfg->target_agent < 0 || cfg->target_agent >= A)) {
+        set_err("maze navigation needs nav_agent/target_agent");
+        return GW_E_INVALID;
+    }
+    if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); return GW_E_HIP; }
+
+    gw_engine* g = new gw_engine();
+    memset(&g->base, 0, sizeof(Params));
+    g->device = device; g->E = n_envs; g->A = A; g->H = cfg->rows; g->W = cfg->cols;
+    g->S = 2 * cfg->obs_range + 1; g->max_enc = max_enc;
+    const size_t EA = (size_t)n_envs * A;
+    Params& p = g->base;
+    HIPCHK(hipMalloc(&p.pos, EA * sizeof(int2)));
+    HIPCHK(hipMalloc(&p.health, EA * sizeof(double)));
+    HIPCHK(hipMalloc(&p.flags, EA));
+    HIPCHK(hipMalloc(&p.seq, EA * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&p.mt, (size_t)n_envs * GW_MT_STRIDE * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&p.steps, (size_t)n_envs * sizeof(int32_t)));
+    HIPCHK(hipMemset(p.pos, 0, EA * sizeof(int2)));
+    HIPCHK(hipMemset(p.health, 0, EA * sizeof(double)));
+    HIPCHK(hipMemset(p.flags, 0, EA));
+    HIPCHK(hipMemset(p.seq, 0, EA * sizeof(uint32_t)));
+    HIPCHK(hipMemset(p.mt, 0, (size_t)n_envs * GW_MT_STRIDE * sizeof(uint32_t)));
+    HIPCHK(hipMemset(p.steps, 0, (size_t)n_envs * sizeof(int32_t)));
+    DevAgent hs[GW_MAX_AGENTS];
+    for (int a = 0; a < A; a++) {
+        const gw_agent_spec& s = cfg->agents[a];
+        hs[a].enc = s.encoding; hs[a].kind = s.kind; hs[a].init_r = s.init_row; hs[a].init_c = s.init_col;
+        hs[a].view_range = s.view_range; hs[a].move_range = s.move_range;
+        hs[a].attack_range = s.attack_range; hs[a].simul = s.simultaneous_attacks;
+        hs[a].strength = s.attack_strength; hs[a].accuracy = s.attack_accuracy;
+        hs[a].init_health = s.initial_health;
+    }
+    HIPCHK(hipMalloc(&g->d_spec, sizeof(DevAgent) * A));
+    HIPCHK(hipMemcpy(g->d_spec, hs, sizeof(DevAgent) * A, hipMemcpyHostToDevice));
+    p.spec = g->d_spec;
+    p.E = n_envs; p.A = A; p.H = cfg->rows; p.W = cfg->cols; p.max_enc = max_enc;
+    p.sim_kind = cfg->sim_kind; p.nav = cfg->nav_agent; p.target = cfg->target_agent;
+    p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
+    p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
+    p.done_kind = cfg->done_kind;
+    for (int i = 0; i <= GW_MAX_ENC; i++) { p.overlap[i] = cfg->overlap[i]; p.amap[i] = cfg->attack_mapping[i]; }
+    const int SS = g->S * g->S;
+    g->smem_step = smem_bytes(HW, A, SS, max_enc, false);
+    g->smem_reset = smem_bytes(HW, A, SS, max_enc, true);
+    HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
+    *out = g;
+    return GW_OK;
+}
+
+gw_status gw_destroy(gw_handle g)
+{
+    if (!g) return GW_E_INVALID;
+    hipFree(g->base.pos); hipFree(g->base.health); hipFree(g->base.flags); hipFree(g->base.seq);
+    hipFree(g->base.mt); hipFree(g->base.steps); hipFree(g->d_spec);
+    delete g;
+    return GW_OK;
+}
+
+int32_t gw_num_envs(gw_handle g) { return g ? g->E : 0; }
+int32_t gw_obs_side(gw_handle g) { return g ? g->S : 0; }
+
+gw_status gw_seed(gw_handle g, const uint32_t* seeds, void* stream)
+{
+    if (!g || !seeds) return GW_E_INVALID;
+    hipLaunchKernelGGL(seed_kernel, dim3((g->E + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       g->base.mt, seeds, g->E);
+    HIPCHK(hipGetLastError());
+    return GW_OK;
+}
+
+gw_status gw_reset(gw_handle g, const uint8_t* mask, const uint8_t* all_done, int32_t horizon,
+                   int32_t* obs, uint32_t* err_flags, void* stream)
+{
+    if (!g || !obs) return GW_E_INVALID;
+    Params p = g->base;
+    p.mask = mask; p.prev_all_done = all_done; p.horizon = horizon; p.obs = obs; p.err = err_flags;
+    HIPCHK(do_reset(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_step(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
+                  uint8_t* done, uint8_t* all_done, uint64_t* acting, void* stream)
+{
+    if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.acting = acting;
+    HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_get_state(gw_handle g, int32_t* pos, double* health, uint8_t* flags, uint32_t* seq,
+                       uint32_t* mt, int32_t* steps, void* stream)
+{
+    if (!g) return GW_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t EA = (size_t)g->E * g->A;
+    if (pos) HIPCHK(hipMemcpyAsync(pos, g->base.pos, EA * sizeof(int2), hipMemcpyDeviceToDevice, st));
+    if (health) HIPCHK(hipMemcpyAsync(health, g->base.health, EA * 8, hipMemcpyDeviceToDevice, st));
+    if (flags) HIPCHK(hipMemcpyAsync(flags, g->base.flags, EA, hipMemcpyDeviceToDevice, st));
+    if (seq) HIPCHK(hipMemcpyAsync(seq, g->base.seq, EA * 4, hipMemcpyDeviceToDevice, st));
+    if (mt) HIPCHK(hipMemcpyAsync(mt, g->base.mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
+    if (steps) HIPCHK(hipMemcpyAsync(steps, g->base.steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
+gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, const uint8_t* flags,
+                       const uint32_t* seq, const uint32_t* mt, const int32_t* steps, void* stream)
+{
+    if (!g) return GW_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t EA = (size_t)g->E * g->A;
+    if (pos) HIPCHK(hipMemcpyAsync(g->base.pos, pos, EA * sizeof(int2), hipMemcpyDeviceToDevice, st));
+    if (health) HIPCHK(hipMemcpyAsync(g->base.health, health, EA * 8, hipMemcpyDeviceToDevice, st));
+    if (flags) HIPCHK(hipMemcpyAsync(g->base.flags, flags, EA, hipMemcpyDeviceToDevice, st));
+    if (seq) HIPCHK(hipMemcpyAsync(g->base.seq, seq, EA * 4, hipMemcpyDeviceToDevice, st));
+    if (mt) HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
+    if (steps) HIPCHK(hipMemcpyAsync(g->base.steps, steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
+gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, int32_t* actions, void* stream)
+{
+    if (!g || !actions) return GW_E_INVALID;
+    const int n = g->E * g->A;
+    hipLaunchKernelGGL(random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, actions);
+    HIPCHK(hipGetLastError());
+    return GW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Batched tensor API over the HIP engine (one handle = E environments).
+
+All buffers are torch tensors on the engine's device; the C-ABI receives raw
+device pointers and the current HIP stream.  This is the vectorised-env
+surface (RLlib VectorEnv-style): ``reset`` / ``step`` advance every env in
+one kernel launch each, with optional on-device auto-reset.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from abmarl_amd import _abi, _native
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def env_seeds(n_envs, run=0, first_env=0):
+    """Per-env MT19937 seeds, keyed by the GLOBAL env id:
+    seed_e = 1_000_003 * run + e  (mod 2^32)."""
+    e = np.arange(first_env, first_env + n_envs, dtype=np.uint64)
+    return ((np.uint64(1_000_003) * np.uint64(run) + e) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+class GridWorldEngine:
+    def __init__(self, compiled, n_envs, device=None, seeds=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("GridWorldEngine needs a ROCm GPU (no CPU fallback).")
+        self.L = _native.lib()
+        self.cc = compiled
+        self.device = torch.device(device if device is not None else 'cuda')
+        if self.device.index is None:
+            self.device = torch.device('cuda', torch.cuda.current_device())
+        self.E, self.A, self.S = int(n_envs), compiled.n_agents, compiled.obs_side
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_create(C.cast(C.byref(compiled.cfg), C.c_void_p), self.E,
+                                           self.device.index, C.byref(h)), 'gw_create')
+        self.h = h
+        dev = self.device
+        E, A, S = self.E, self.A, self.S
+        self.obs = torch.full((E, A, S, S), -2, dtype=torch.int32, device=dev)
+        self.reward = torch.zeros((E, A), dtype=torch.float64, device=dev)
+        self.done = torch.ones((E, A), dtype=torch.uint8, device=dev)
+        self.all_done = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        self.err = torch.zeros((E,), dtype=torch.int32, device=dev)
+        self.acting = torch.zeros((E,), dtype=torch.int64, device=dev)
+        self.actions = torch.zeros((E, A, _abi.GW_ACT_DIM), dtype=torch.int32, device=dev)
+        self.seed(env_seeds(E) if seeds is None else seeds)
+
+    def __del__(self):
+        h = getattr(self, 'h', None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.device)
+                self.L.gw_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    # ------------------------------------------------------------ control
+    def seed(self, seeds):
+        s = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32),
+                            device=self.device)
+        assert s.numel() == self.E
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_seed(self.h, _ptr(s), _stream()), 'gw_seed')
+            torch.cuda.current_stream().synchronize()
+
+    def reset(self, mask=None, all_done=None, horizon=0, obs=None):
+        """Reset selected envs (all of them by default); returns the obs buffer."""
+        out = self.obs if obs is None else obs
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_reset(self.h, _ptr(mask), _ptr(all_done), int(horizon),
+                                          _ptr(out), _ptr(self.err), _stream()), 'gw_reset')
+        return out
+
+    def step(self, actions=None):
+        """One AllStepManager.step on every env; returns (obs, reward, done, all_done)."""
+        a = self.actions if actions is None else actions
+        assert a.dtype == torch.int32 and a.is_contiguous() and a.shape == self.actions.shape
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
+                                         _ptr(self.done), _ptr(self.all_done), _ptr(self.acting),
+                                         _stream()), 'gw_step')
+        return self.obs, self.reward, self.done, self.all_done
+
+    def random_actions(self, key, step, out=None):
+        """Synthetic random policy (Philox, keyed by key/env/step/agent)."""
+        out = self.actions if out is None else out
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_random_actions(self.h, int(key) & 0xFFFFFFFFFFFFFFFF,
+                                                   int(step) & 0xFFFFFFFF, _ptr(out), _stream()),
+                          'gw_random_actions')
+        return out
+
+    def check_errors(self):
+        err = self.err.cpu().numpy()
+        if (err & _abi.GW_ERR_NO_CELL).any():
+            e = int(np.nonzero(err & _abi.GW_ERR_NO_CELL)[0][0])
+            raise RuntimeError(f"Could not find a cell for an agent (env {e})")
+        if (err & _abi.GW_ERR_INIT_POSITION).any():
+            e = int(np.nonzero(err & _abi.GW_ERR_INIT_POSITION)[0][0])
+            raise AssertionError(f"Initial cell not available (env {e})")
+
+    # ------------------------------------------------------------ state
+    def get_state(self):
+        E, A, dev = self.E, self.A, self.device
+        st = dict(pos=torch.zeros((E, A, 2), dtype=torch.int32, device=dev),
+                  health=torch.zeros((E, A), dtype=torch.float64, device=dev),
+                  flags=torch.zeros((E, A), dtype=torch.uint8, device=dev),
+                  seq=torch.zeros((E, A), dtype=torch.int32, device=dev),
+                  mt=torch.zeros((E, _abi.GW_MT_STRIDE), dtype=torch.int32, device=dev),
+                  steps=torch.zeros((E,), dtype=torch.int32, device=dev))
+        with torch.cuda.device(dev):
+            _native.check(self.L.gw_get_state(self.h, *[_ptr(st[k]) for k in
+                                                        ('pos', 'health', 'flags', 'seq', 'mt',
+                                                         'steps')], _stream()), 'gw_get_state')
+        return st
+
+    def set_state(self, pos=None, health=None, flags=None, seq=None, mt=None, steps=None):
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_set_state(self.h, _ptr(pos), _ptr(health), _ptr(flags),
+                                              _ptr(seq), _ptr(mt), _ptr(steps), _stream()),
+                          'gw_set_state')

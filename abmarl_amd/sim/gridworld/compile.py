@@ -1,0 +1,134 @@
+"""Compile a host-side GridWorld simulation into the engine's gw_config.
+
+Every value the reference reads from Python objects inside its step loop is
+lowered here, once, to constant tables:
+  agents dict order          -> entity index (the reference iterates dicts in
+                                insertion order everywhere: team_battle_example.py:35,
+                                all_step_manager.py:68-83)
+  isinstance checks          -> kind bits (GW_K_*)
+  Grid.overlapping (sym.)    -> overlap bitmask per encoding (grid.py:53-71,95-103)
+  attack_mapping             -> bitmask per encoding (actor.py:385)
+  component flags            -> stacked_attacks / observe_self / no_overlap_at_reset
+  SmartGWS._states set order -> state_order (pinned)
+"""
+from abmarl_amd import _abi
+from abmarl_amd.sim.agent_based_simulation import ObservingAgent, ActingAgent
+from abmarl_amd.sim.gridworld.agent import (
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
+from abmarl_amd.sim.gridworld.components import (
+    PositionState, HealthState, BinaryAttackActor, PositionCenteredEncodingObserver,
+    ActiveDone, OneTeamRemainingDone, MoveActor)
+
+
+class UnsupportedConfig(ValueError):
+    pass
+
+
+def agent_spec(agent):
+    kind = 0
+    if isinstance(agent, ObservingAgent):
+        kind |= _abi.GW_K_OBSERVING
+    if isinstance(agent, ActingAgent):
+        kind |= _abi.GW_K_ACTING
+    if isinstance(agent, GridObservingAgent):
+        kind |= _abi.GW_K_GRID_OBSERVER
+    if isinstance(agent, MovingAgent):
+        kind |= _abi.GW_K_MOVING
+    if isinstance(agent, AttackingAgent):
+        kind |= _abi.GW_K_ATTACKING
+    if isinstance(agent, HealthAgent):
+        kind |= _abi.GW_K_HEALTH
+    if agent.blocking:
+        kind |= _abi.GW_K_BLOCKING
+    s = _abi.AgentSpec()
+    s.encoding = agent.encoding
+    s.kind = kind
+    if agent.initial_position is not None:
+        s.init_row, s.init_col = int(agent.initial_position[0]), int(agent.initial_position[1])
+    else:
+        s.init_row = s.init_col = -1
+    s.view_range = getattr(agent, 'view_range', 0) or 0
+    s.move_range = getattr(agent, 'move_range', 0) or 0
+    s.attack_range = getattr(agent, 'attack_range', 0) or 0
+    s.simultaneous_attacks = getattr(agent, 'simultaneous_attacks', 0) or 0
+    s.attack_strength = float(getattr(agent, 'attack_strength', 0) or 0)
+    s.attack_accuracy = float(getattr(agent, 'attack_accuracy', 0) or 0)
+    ih = getattr(agent, 'initial_health', None)
+    s.initial_health = -1.0 if ih is None else float(ih)
+    return s
+
+
+def compile_sim(sim, program, states, observers, dones, actors, state_order,
+                nav_agent=-1, target_agent=-1):
+    agents = list(sim.agents.values())
+    for a in agents:
+        if not isinstance(a, GridWorldAgent):
+            raise UnsupportedConfig(f"{a.id} is not a GridWorldAgent")
+    n = len(agents)
+    if n == 0:
+        raise UnsupportedConfig("no agents")
+    encs = [a.encoding for a in agents]
+    if min(encs) < 1 or max(encs) > _abi.GW_MAX_ENC:
+        raise UnsupportedConfig(f"encodings must be in 1..{_abi.GW_MAX_ENC}")
+    if sim.grid.rows * sim.grid.cols > _abi.GW_MAX_CELLS:
+        raise UnsupportedConfig(f"grid larger than {_abi.GW_MAX_CELLS} cells")
+
+    pos_states = [s for s in states if isinstance(s, PositionState)]
+    health_states = [s for s in states if isinstance(s, HealthState)]
+    if len(pos_states) != 1:
+        raise UnsupportedConfig("exactly one PositionState is required")
+    if any(isinstance(a, HealthAgent) for a in agents) and not health_states:
+        raise UnsupportedConfig("HealthAgents require a HealthState")
+    if pos_states[0].randomize_placement_order:
+        raise UnsupportedConfig("randomize_placement_order (Python random.shuffle) is not "
+                                "reproduced by the engine")
+
+    obs_range = 0
+    observe_self = True
+    pco = [o for o in observers if isinstance(o, PositionCenteredEncodingObserver)]
+    if len(pco) != len(observers) or len(pco) > 1:
+        raise UnsupportedConfig("the engine implements one PositionCenteredEncodingObserver")
+    ranges = {a.view_range for a in agents if isinstance(a, GridObservingAgent)}
+    if pco:
+        observe_self = pco[0].observe_self
+        if len(ranges) > 1:
+            raise UnsupportedConfig("all GridObservingAgents must share one view_range")
+        obs_range = ranges.pop() if ranges else 0
+    if obs_range > _abi.GW_MAX_RANGE:
+        raise UnsupportedConfig(f"view_range > {_abi.GW_MAX_RANGE}")
+
+    attack = [x for x in actors if isinstance(x, BinaryAttackActor)]
+    amap = {}
+    stacked = False
+    if attack:
+        stacked = attack[0].stacked_attacks
+        for k, v in attack[0].attack_mapping.items():
+            if 1 <= k <= _abi.GW_MAX_ENC:
+                amap[k] = sum(1 << e for e in v if 1 <= e <= _abi.GW_MAX_ENC)
+        for a in agents:
+            if isinstance(a, AttackingAgent):
+                if a.encoding not in attack[0].attack_mapping:
+                    # the reference raises KeyError at actor.py:385 on the first candidate
+                    raise UnsupportedConfig(f"{a.id}'s encoding is not in attack_mapping")
+                if a.attack_range > _abi.GW_MAX_RANGE:
+                    raise UnsupportedConfig(f"attack_range > {_abi.GW_MAX_RANGE}")
+    for x in actors:
+        if not isinstance(x, (BinaryAttackActor, MoveActor)):
+            raise UnsupportedConfig(f"{type(x).__name__} has no HIP implementation")
+
+    done_kind = 0
+    for d in dones:
+        if isinstance(d, OneTeamRemainingDone):
+            done_kind |= _abi.GW_DONE_ONE_TEAM
+        elif isinstance(d, ActiveDone):
+            done_kind |= _abi.GW_DONE_ACTIVE
+        else:
+            raise UnsupportedConfig(f"{type(d).__name__} has no HIP implementation")
+    # OneTeamRemainingDone.get_done is ActiveDone.get_done (done.py:140)
+    order = {'position_health': _abi.GW_ORDER_POSITION_HEALTH,
+             'health_position': _abi.GW_ORDER_HEALTH_POSITION}[state_order]
+    return _abi.CompiledConfig(
+        sim.grid.rows, sim.grid.cols, [agent_spec(a) for a in agents], program,
+        sim.grid.overlap_bits(), amap, stacked_attacks=stacked, observe_self=observe_self,
+        no_overlap_at_reset=pos_states[0].no_overlap_at_reset, state_order=order,
+        done_kind=done_kind, obs_range=obs_range, nav_agent=nav_agent, target_agent=target_agent)

@@ -1,0 +1,185 @@
+"""State / Actor / Observer / Done components (the reference's plugin API).
+
+Each class keeps the reference's name, constructor arguments, validation and
+space assignment; its per-agent Python body is executed by the engine's
+fused HIP step instead of here.  What each one contributes to the compiled
+engine configuration is in ``abmarl_amd/sim/gridworld/compile.py``.
+
+Reference: abmarl/sim/gridworld/state.py:13-166,622-641; actor.py:13-114,
+237-501; observer.py:13-52,153-250; done.py:10-56,140-153.
+"""
+from abc import ABC, abstractmethod
+
+import numpy as np
+
+from abmarl_amd.spaces import Box, Discrete
+from abmarl_amd.sim.gridworld.base import GridWorldBaseComponent
+from abmarl_amd.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent
+
+
+class _EngineExecuted:
+    def _engine_only(self, name):
+        raise RuntimeError(
+            f"{type(self).__name__}.{name} runs inside the fused HIP step; drive the simulation "
+            "through its manager (AllStepManager / MultiAgentWrapper) or GridWorldEngine.")
+
+
+# ----------------------------------------------------------------- states
+class StateBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
+    """state.py:13-22."""
+
+    def reset(self, **kwargs):
+        self._engine_only('reset')
+
+
+class PositionState(StateBaseComponent):
+    """state.py:25-166: initial positions first, then random cells drawn from
+    per-encoding ordered availability lists (np.random.choice)."""
+
+    def __init__(self, no_overlap_at_reset=False, randomize_placement_order=False, **kwargs):
+        super().__init__(**kwargs)
+        assert type(no_overlap_at_reset) is bool, "No overlap at reset must be a boolean."
+        assert type(randomize_placement_order) is bool, \
+            "Randomize placement order must be True or False."
+        self.no_overlap_at_reset = no_overlap_at_reset
+        self.randomize_placement_order = randomize_placement_order
+
+
+class HealthState(StateBaseComponent):
+    """state.py:622-641: initial_health or np.random.uniform(0, 1)."""
+
+
+# ----------------------------------------------------------------- actors
+class ActorBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
+    """actor.py:13-52."""
+
+    def process_action(self, agent, action_dict, **kwargs):
+        self._engine_only('process_action')
+
+    @property
+    @abstractmethod
+    def key(self):
+        pass
+
+    @property
+    @abstractmethod
+    def supported_agent_type(self):
+        pass
+
+
+class MoveActor(ActorBaseComponent):
+    """actor.py:55-114: action space Box(-move_range, move_range, (2,), int)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        for agent in self.agents.values():
+            if isinstance(agent, self.supported_agent_type):
+                agent.action_space[self.key] = Box(-agent.move_range, agent.move_range, (2,), int)
+                agent.null_action[self.key] = np.zeros((2,), dtype=int)
+
+    @property
+    def key(self):
+        return 'move'
+
+    @property
+    def supported_agent_type(self):
+        return MovingAgent
+
+
+class AttackActorBaseComponent(ActorBaseComponent, ABC):
+    """actor.py:237-438."""
+
+    def __init__(self, attack_mapping=None, stacked_attacks=False, **kwargs):
+        super().__init__(**kwargs)
+        assert type(attack_mapping) is dict, "Attack mapping must be dictionary."
+        for k, v in attack_mapping.items():
+            assert type(k) is int, "All keys in attack mapping must be an integer."
+            assert type(v) is set, "All values in attack mapping must be a set."
+            for i in v:
+                assert type(i) is int, "All elements in the attack mapping values must be integers."
+        assert type(stacked_attacks) is bool, "Stacked attacks must be a boolean."
+        self.attack_mapping = attack_mapping
+        self.stacked_attacks = stacked_attacks
+        for agent in self.agents.values():
+            if isinstance(agent, self.supported_agent_type):
+                self._assign_space(agent)
+
+    @property
+    def key(self):
+        return 'attack'
+
+    @property
+    def supported_agent_type(self):
+        return AttackingAgent
+
+    @abstractmethod
+    def _assign_space(self, agent):
+        pass
+
+
+class BinaryAttackActor(AttackActorBaseComponent):
+    """actor.py:441-501: Discrete(simultaneous_attacks + 1) attacks in the local grid."""
+
+    def _assign_space(self, agent):
+        agent.action_space[self.key] = Discrete(agent.simultaneous_attacks + 1)
+        agent.null_action[self.key] = 0
+
+
+# -------------------------------------------------------------- observers
+class ObserverBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
+    """observer.py:13-52."""
+
+    def get_obs(self, agent, **kwargs):
+        self._engine_only('get_obs')
+
+    @property
+    @abstractmethod
+    def key(self):
+        pass
+
+    @property
+    @abstractmethod
+    def supported_agent_type(self):
+        pass
+
+
+class PositionCenteredEncodingObserver(ObserverBaseComponent):
+    """observer.py:153-250: Box(-2, max_encoding, (2v+1, 2v+1), int)."""
+
+    def __init__(self, observe_self=True, **kwargs):
+        super().__init__(**kwargs)
+        assert type(observe_self) is bool, "Observe self must be a boolean."
+        self.observe_self = observe_self
+        max_encoding = max(agent.encoding for agent in self.agents.values())
+        for agent in self.agents.values():
+            if isinstance(agent, self.supported_agent_type):
+                side = agent.view_range * 2 + 1
+                agent.observation_space[self.key] = Box(-2, max_encoding, (side, side), int)
+                agent.null_observation[self.key] = -2 * np.ones((side, side), dtype=int)
+
+    @property
+    def key(self):
+        return 'position_centered_encoding'
+
+    @property
+    def supported_agent_type(self):
+        return GridObservingAgent
+
+
+# ------------------------------------------------------------------ dones
+class DoneBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
+    """done.py:10-36."""
+
+    def get_done(self, agent, **kwargs):
+        self._engine_only('get_done')
+
+    def get_all_done(self, **kwargs):
+        self._engine_only('get_all_done')
+
+
+class ActiveDone(DoneBaseComponent):
+    """done.py:39-56: done = not active; all done = no active agent."""
+
+
+class OneTeamRemainingDone(ActiveDone):
+    """done.py:140-153: all done when the active agents share <= 1 encoding."""

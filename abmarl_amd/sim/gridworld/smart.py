@@ -1,0 +1,123 @@
+"""SmartGridWorldSimulation backed by the HIP engine.
+
+Reference: abmarl/sim/gridworld/smart.py:10-120.  Components are given as sets
+of registered names or classes exactly as in the reference.  Because the
+reference stores the state components in a Python ``set`` (smart.py:37), the
+order in which PositionState and HealthState draw from the RNG at reset is
+set-iteration order there; here it is pinned by ``state_order``
+('position_health' by default, or 'health_position').
+
+Runtime: the simulation compiles itself to a ``gw_config`` and runs on a
+one-env ``GridWorldEngine``.  The engine fuses the AllStepManager protocol
+(step -> obs -> rewards -> dones -> done_agents, all_step_manager.py:51-95)
+into one kernel, so ``step`` computes every live agent's observation, reward
+and done at once and ``get_obs`` / ``get_reward`` / ``get_done`` return those
+results.  The global numpy legacy RNG (np.random) is carried through the
+engine on every call (its MT19937 state is uploaded before and read back
+after), so a sim driven by AllStepManager consumes and produces exactly what
+the reference would from the same np.random.seed.
+"""
+from abc import ABC
+
+import numpy as np
+
+from abmarl_amd import _abi
+from abmarl_amd.sim.agent_based_simulation import Agent
+from abmarl_amd.sim.gridworld.base import GridWorldSimulation
+from abmarl_amd.sim.gridworld.components import (
+    StateBaseComponent, ObserverBaseComponent, DoneBaseComponent, ActorBaseComponent)
+from abmarl_amd.sim.gridworld.registry import registry
+from abmarl_amd.sim.gridworld.compile import compile_sim
+
+
+def _build_components(items, kind, base, kwargs):
+    assert type(items) is set, f"{kind.capitalize()}s must be a set of {kind} components"
+    out = []
+    # deterministic order: by class name (the reference's order is set order)
+    resolved = []
+    for item in items:
+        if type(item) is str:
+            assert item in registry[kind], f"{item} is not registered as a {kind}."
+            resolved.append(registry[kind][item])
+        elif isinstance(item, type) and issubclass(item, base):
+            resolved.append(item)
+        else:
+            raise ValueError(f"{item} must be a {kind} component or the name of a registered "
+                             f"{kind} component.")
+    for cls in sorted(resolved, key=lambda c: c.__name__):
+        out.append(cls(**kwargs))
+    return out
+
+
+class SmartGridWorldSimulation(GridWorldSimulation, ABC):
+    # engine program implementing this class's step(); set by subclasses
+    _engine_program = None
+
+    def __init__(self, states=None, observers=None, dones=None, state_order='position_health',
+                 device=None, **kwargs):
+        super().__init__(**kwargs)
+        self._states = _build_components(states, 'state', StateBaseComponent, kwargs) \
+            if states else []
+        self._observers = _build_components(observers, 'observer', ObserverBaseComponent,
+                                            kwargs) if observers else []
+        self._dones = _build_components(dones, 'done', DoneBaseComponent, kwargs) \
+            if dones else []
+        assert state_order in ('position_health', 'health_position'), \
+            "state_order must be 'position_health' or 'health_position'"
+        self.state_order = state_order
+        self._device = device
+        self._runtime = None
+        self.rewards = {}
+
+    # ------------------------------------------------------------ compile
+    def _actors(self):
+        return [v for v in vars(self).values() if isinstance(v, ActorBaseComponent)]
+
+    def _program_extras(self):
+        return {}
+
+    def compiled(self):
+        """This simulation as an engine configuration (_abi.CompiledConfig)."""
+        assert self._engine_program is not None, \
+            f"{type(self).__name__} has no engine step program"
+        return compile_sim(self, self._engine_program, self._states, self._observers,
+                           self._dones, self._actors(), self.state_order,
+                           **self._program_extras())
+
+    def _rt(self):
+        if self._runtime is None:
+            from abmarl_amd.sim.gridworld.runtime import DictRuntime
+            self._runtime = DictRuntime(self, self.compiled(), self._device)
+        return self._runtime
+
+    # ------------------------------------------------------------ ABS API
+    def reset(self, **kwargs):
+        assert self._states, "Smart Simulation requires '_states' attribute."
+        self._rt().reset()
+        self.rewards = {a.id: 0 for a in self.agents.values() if isinstance(a, Agent)}
+
+    def step(self, action_dict, **kwargs):
+        self._rt().step(action_dict)
+
+    def get_obs(self, agent_id, **kwargs):
+        assert self._observers, "Smart Simulation requires '_observers' attribute."
+        return self._rt().get_obs(agent_id)
+
+    def get_reward(self, agent_id, **kwargs):
+        return self._rt().get_reward(agent_id)
+
+    def get_done(self, agent_id, **kwargs):
+        assert self._dones, "Smart Simulation requires '_dones' attribute."
+        return self._rt().get_done(agent_id)
+
+    def get_all_done(self, **kwargs):
+        assert self._dones, "Smart Simulation requires '_dones' attribute."
+        return self._rt().get_all_done()
+
+    def get_info(self, agent_id, **kwargs):
+        return {}
+
+    @property
+    def done_agents(self):
+        """Agents the fused manager protocol considers done."""
+        return self._rt().done_agents()

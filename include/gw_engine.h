@@ -1,0 +1,188 @@
+/*
+ * gw_engine.h — C-ABI of the MI355X batched GridWorld step engine.
+ *
+ * This is the drop-in boundary for Abmarl's GridWorld hot path.  One handle
+ * holds E independent environments of one simulation configuration; every
+ * call advances all (or a masked subset of) them on one HIP stream.
+ *
+ * Reference interfaces each entry point replaces (paths under
+ * gillette7/Abmarl, abmarl/):
+ *
+ *   gw_create   GridWorldSimulation.build_sim          sim/gridworld/base.py:38-59
+ *               + SmartGridWorldSimulation.__init__     sim/gridworld/smart.py:26-84
+ *               + AllStepManager.__init__               managers/all_step_manager.py:8-17
+ *   gw_seed     np.random.seed(seed) per env            (numpy legacy MT19937 init_genrand)
+ *   gw_reset    AllStepManager.reset                    managers/all_step_manager.py:37-49
+ *               -> SmartGridWorldSimulation.reset       sim/gridworld/smart.py:86-91
+ *                  -> PositionState.reset               sim/gridworld/state.py:88-166
+ *                  -> HealthState.reset                 sim/gridworld/state.py:629-641
+ *               -> get_obs for every live agent         sim/gridworld/observer.py:204-250
+ *   gw_step     AllStepManager.step                     managers/all_step_manager.py:51-95
+ *               -> TeamBattleSim.step                   examples/sim/team_battle_example.py:33-59
+ *                  -> BinaryAttackActor.process_action  sim/gridworld/actor.py:306-361,455-501
+ *                  -> MoveActor.process_action          sim/gridworld/actor.py:82-114
+ *               -> MazeNavigationSim.step               examples/sim/maze_navigation.py:25-42
+ *               -> get_obs / get_reward / get_done      sim/gridworld/smart.py:93-117
+ *                  -> ActiveDone / OneTeamRemainingDone sim/gridworld/done.py:39-56,140-153
+ *   gw_get_state / gw_set_state   (no reference equivalent: engine SoA snapshot,
+ *               used for checkpoint and for parity tests)
+ *   gw_destroy  (Python GC of the simulation objects)
+ *
+ * Conventions
+ *   - All I/O buffers are caller-owned DEVICE pointers (allocated by the
+ *     caller, e.g. torch).  The engine owns only its internal state.
+ *   - Calls are stream-ordered on the `stream` argument (a hipStream_t, 0 =
+ *     default stream) and are not re-entrant per handle.
+ *   - Return value: GW_OK or a negative gw_status.  Per-env failures that the
+ *     reference raises as Python exceptions are reported in err_flags[E]
+ *     (GW_ERR_*); the Python facade maps them back to the same exception types.
+ *   - No torch / HIP types appear in the signatures: streams are void*.
+ */
+#ifndef GW_ENGINE_H
+#define GW_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ limits */
+#define GW_MAX_AGENTS   64   /* one wavefront lane per entity (engine)        */
+#define GW_MAX_ENC      15   /* encodings 1..15                               */
+#define GW_MAX_CELLS  4096   /* rows*cols                                     */
+#define GW_MAX_RANGE     7   /* view / attack range                           */
+#define GW_ACT_DIM       3   /* actions[e][a] = {move_row, move_col, attack}  */
+#define GW_MT_N        624   /* MT19937 state words                           */
+#define GW_MT_STRIDE   640   /* words per env in the MT state array (624 key + pos, padded) */
+
+/* ----------------------------------------------------------- status codes */
+typedef int32_t gw_status;
+#define GW_OK               0
+#define GW_E_INVALID      (-1)  /* bad config / argument                  */
+#define GW_E_HIP          (-2)  /* HIP runtime error                      */
+#define GW_E_UNSUPPORTED  (-3)  /* config outside what the engine builds  */
+
+/* per-env error flags (err_flags[e], OR-ed) */
+#define GW_ERR_NO_CELL        1u  /* PositionState: RuntimeError "Could not find a cell"  state.py:158-162 */
+#define GW_ERR_INIT_POSITION  2u  /* PositionState: AssertionError initial cell taken     state.py:147-149 */
+
+/* ------------------------------------------------------------ agent kinds */
+/* bit flags describing which reference mixins an entity derives from        */
+#define GW_K_OBSERVING     0x01u /* ObservingAgent            agent_based_simulation.py:120 */
+#define GW_K_ACTING        0x02u /* ActingAgent               agent_based_simulation.py:66  */
+#define GW_K_GRID_OBSERVER 0x04u /* GridObservingAgent        gridworld/agent.py:122         */
+#define GW_K_MOVING        0x08u /* MovingAgent               gridworld/agent.py:147         */
+#define GW_K_ATTACKING     0x10u /* AttackingAgent            gridworld/agent.py:213         */
+#define GW_K_HEALTH        0x20u /* HealthAgent               gridworld/agent.py:172         */
+#define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75       */
+
+/* ---------------------------------------------------------- sim programs */
+#define GW_SIM_TEAM_BATTLE  1   /* examples/sim/team_battle_example.py:33-59 */
+#define GW_SIM_MAZE_NAV     2   /* examples/sim/maze_navigation.py:25-42     */
+
+/* done components (bit set; get_done = AND, get_all_done = AND: smart.py:106-117) */
+#define GW_DONE_ACTIVE        0x1u /* ActiveDone            done.py:39-56   */
+#define GW_DONE_ONE_TEAM      0x2u /* OneTeamRemainingDone  done.py:140-153 */
+
+/* reset-time state component order (SmartGridWorldSimulation iterates a set) */
+#define GW_ORDER_POSITION_HEALTH 0
+#define GW_ORDER_HEALTH_POSITION 1
+
+typedef struct gw_agent_spec {
+    int32_t  encoding;             /* >= 1                                     */
+    uint32_t kind;                 /* GW_K_* bits                              */
+    int32_t  init_row, init_col;   /* initial_position, or -1,-1 for random    */
+    int32_t  view_range;
+    int32_t  move_range;
+    int32_t  attack_range;
+    int32_t  simultaneous_attacks;
+    double   attack_strength;
+    double   attack_accuracy;
+    double   initial_health;       /* < 0 means None (uniform(0,1) at reset)   */
+} gw_agent_spec;
+
+typedef struct gw_config {
+    int32_t  rows, cols;
+    int32_t  n_agents;             /* entities, in agents-dict order            */
+    int32_t  sim_kind;             /* GW_SIM_*                                  */
+    /* overlap[e] bit f set <=> encoding e may share a cell with encoding f
+       (already made symmetric, grid.py:53-71; missing key == empty set)       */
+    uint32_t overlap[GW_MAX_ENC + 1];
+    /* attack_mapping[e] bit f set <=> e may attack f (actor.py:278-287)       */
+    uint32_t attack_mapping[GW_MAX_ENC + 1];
+    int32_t  stacked_attacks;      /* AttackActorBaseComponent.stacked_attacks  */
+    int32_t  observe_self;         /* PositionCenteredEncodingObserver          */
+    int32_t  no_overlap_at_reset;  /* PositionState                             */
+    int32_t  state_order;          /* GW_ORDER_*                                */
+    uint32_t done_kind;            /* GW_DONE_* bits                            */
+    int32_t  obs_range;            /* shared view_range of every grid observer  */
+    int32_t  target_agent;         /* MazeNav: index of 'target' (else -1)      */
+    int32_t  nav_agent;            /* MazeNav: index of 'navigator' (else -1)   */
+    const gw_agent_spec* agents;   /* host pointer, n_agents entries            */
+} gw_config;
+
+typedef struct gw_engine* gw_handle;
+
+/* Build an engine for n_envs environments of `cfg` on HIP device `device`.
+   Validates the config against the engine's limits (GW_E_UNSUPPORTED).     */
+gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out);
+
+/* Seed env e's MT19937 with seeds[e] (np.random.seed semantics).
+   seeds: device uint32[E].                                                   */
+gw_status gw_seed(gw_handle h, const uint32_t* seeds, void* stream);
+
+/* Reset the selected envs: all of them when mask, all_done and horizon are
+   all unset (NULL, NULL, <= 0); otherwise every env e with mask[e] != 0, or
+   all_done[e] != 0 (the previous step's __all__), or steps[e] >= horizon.
+   Writes the reset observation of every entity of the reset envs into obs
+   (untouched for other envs).
+     mask      device uint8[E] or NULL
+     all_done  device uint8[E] or NULL  (the previous step's __all__)
+     obs       device int32[E][A][S][S], S = 2*obs_range+1
+     err_flags device uint32[E] (OR-ed GW_ERR_*)                              */
+gw_status gw_reset(gw_handle h, const uint8_t* mask, const uint8_t* all_done,
+                   int32_t horizon, int32_t* obs, uint32_t* err_flags, void* stream);
+
+/* One AllStepManager.step for every env.
+     actions   device int32[E][A][GW_ACT_DIM]  (ignored for done entities)
+     obs       device int32[E][A][S][S]  (-2 for entities that are done)
+     reward    device double[E][A]      (0 for entities that are done)
+     done      device uint8[E][A]       (1 for entities that were already done)
+     all_done  device uint8[E]          ('__all__')
+     acting    device uint64[E] or NULL (+= number of acting agents, for metrics) */
+gw_status gw_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
+                  uint8_t* done, uint8_t* all_done, uint64_t* acting, void* stream);
+
+/* Snapshot / restore of the engine state (device buffers, caller-owned).
+     pos     int32[E][A][2]   (row, col)
+     health  double[E][A]
+     flags   uint8[E][A]      bit0 in-grid, bit1 live (not in done_agents), bit2 active
+     seq     uint32[E][A]     placement order inside a cell (dict insertion order)
+     mt      uint32[E][GW_MT_STRIDE]  key[624], pos at [624]
+     steps   int32[E]                                                          */
+gw_status gw_get_state(gw_handle h, int32_t* pos, double* health, uint8_t* flags,
+                       uint32_t* seq, uint32_t* mt, int32_t* steps, void* stream);
+gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
+                       const uint8_t* flags, const uint32_t* seq, const uint32_t* mt,
+                       const int32_t* steps, void* stream);
+
+/* Philox-4x32-10 random policy (uniform over MoveActor Box(-r,r,(2,)) and
+   BinaryAttackActor Discrete(k+1)): actions for every entity of every env,
+   keyed by (key, env, step, agent).  Not part of the reference; it is the
+   benchmark's synthetic policy.                                              */
+gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, int32_t* actions,
+                            void* stream);
+
+gw_status gw_destroy(gw_handle h);
+
+/* Introspection */
+int32_t     gw_num_envs(gw_handle h);
+int32_t     gw_obs_side(gw_handle h);
+const char* gw_last_error(void);
+int32_t     gw_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GW_ENGINE_H */

@@ -1,0 +1,105 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C oracle (gw_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module; the product path (abmarl_amd/) never does.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, 'build', 'libgw_oracle.so')
+
+
+def build(force=False):
+    src = os.path.join(HERE, 'gw_oracle.c')
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call(['make', '-s', '-C', HERE])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB)
+        vp = C.c_void_p
+        L.gwo_create.restype = vp
+        L.gwo_create.argtypes = [vp, C.c_int32]
+        L.gwo_destroy.argtypes = [vp]
+        L.gwo_set_threads.argtypes = [C.c_int32]
+        L.gwo_max_threads.restype = C.c_int32
+        L.gwo_seed.argtypes = [vp, vp]
+        L.gwo_reset.argtypes = [vp, vp, vp, C.c_int32, vp, vp]
+        L.gwo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
+        L.gwo_mt_probe.argtypes = [C.c_uint32, C.c_int32, C.c_uint32, C.c_int32, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Oracle:
+    """Batched CPU oracle with the engine's I/O layout (numpy host arrays)."""
+
+    def __init__(self, compiled, n_envs, threads=None):
+        self.L = lib()
+        self.cc = compiled
+        self.E, self.A, self.S = n_envs, compiled.n_agents, compiled.obs_side
+        if threads:
+            self.L.gwo_set_threads(int(threads))
+        self.h = self.L.gwo_create(C.cast(C.byref(compiled.cfg), C.c_void_p), n_envs)
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.L.gwo_destroy(self.h)
+            self.h = None
+
+    def seed(self, seeds):
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        self.L.gwo_seed(self.h, _p(seeds))
+
+    def new_obs(self):
+        return np.full((self.E, self.A, self.S, self.S), -2, dtype=np.int32)
+
+    def reset(self, obs, mask=None, all_done=None, horizon=0):
+        err = np.zeros(self.E, dtype=np.uint32)
+        mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        all_done = None if all_done is None else np.ascontiguousarray(all_done, dtype=np.uint8)
+        self.L.gwo_reset(self.h, _p(mask), _p(all_done), int(horizon), _p(obs), _p(err))
+        return err
+
+    def step(self, actions, obs, reward, done, all_done, acting=None):
+        actions = np.ascontiguousarray(actions, dtype=np.int32)
+        self.L.gwo_step(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
+                        _p(acting))
+
+    def state(self):
+        E, A = self.E, self.A
+        pos = np.zeros((E, A, 2), np.int32)
+        health = np.zeros((E, A), np.float64)
+        flags = np.zeros((E, A), np.uint8)
+        mt = np.zeros((E, 640), np.uint32)
+        steps = np.zeros(E, np.int32)
+        self.L.gwo_get_state(self.h, _p(pos), _p(health), _p(flags), _p(mt), _p(steps))
+        return dict(pos=pos, health=health, flags=flags, mt=mt, steps=steps)
+
+    def cells(self, env):
+        out = np.zeros((self.cc.rows * self.cc.cols, self.A), np.int32)
+        self.L.gwo_get_cells(self.h, int(env), _p(out))
+        return out
+
+
+def mt_probe(seed, kind, arg, n):
+    out = np.zeros(n, np.float64)
+    lib().gwo_mt_probe(int(seed), int(kind), int(arg), int(n), _p(out))
+    return out

@@ -1,0 +1,212 @@
+"""Generate golden trajectories by running the REFERENCE (gillette7/Abmarl at
+/root/reference) in this container.
+
+Output: tests/golden/<case>.npz — inputs (config, seeds, actions) and the
+reference's outputs (obs, rewards, dones, __all__, positions, health, RNG
+position + key digest) per step.  These are data fixtures; the reference
+source never leaves /root/reference.
+
+Harness contract:
+  * one reference sim + AllStepManager per env, each with its own numpy
+    legacy RNG stream: np.random.seed(seed_e), isolated with get/set_state;
+  * the SmartGridWorldSimulation state components, stored by the reference
+    in a Python set (smart.py:37), are pinned to an explicit order;
+  * identical int actions are fed to every env (generated here with an
+    independent RandomState, stored in the fixture);
+  * auto-reset after a step whose '__all__' is True or when the env reached
+    the horizon, without reseeding (the RNG stream continues).
+
+Run:  python tests/golden/make_golden.py      (needs /root/reference)
+"""
+import json
+import os
+import sys
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get('ABMARL_REFERENCE', '/root/reference')
+
+CASES = [
+    # tiny grid that forces stacks, kills and episode ends
+    dict(name='tb_small', rows=8, cols=8, n_agents=8, n_teams=2, n_envs=6, n_steps=120,
+         horizon=50, seed_base=11),
+    # three teams, cross-team overlap (mixed-encoding cells => the observer's
+    # choice value matters), observe_self=False, partial accuracy, wider ranges
+    dict(name='tb_mixed', rows=7, cols=9, n_agents=12, n_teams=3, n_envs=6, n_steps=120,
+         horizon=40, seed_base=101, overlap={1: [1, 2], 2: [2], 3: [3, 1]},
+         attack_mapping={1: [2, 3], 2: [1, 3], 3: [1, 2]}, observe_self=False,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.6, attack_accuracy=0.7,
+                    view_range=2)),
+    # health first at reset, no_overlap_at_reset, some initial positions/health
+    dict(name='tb_order', rows=6, cols=6, n_agents=10, n_teams=2, n_envs=5, n_steps=100,
+         horizon=30, seed_base=7, state_order='health_position', no_overlap_at_reset=True,
+         initial_positions={0: [0, 0], 3: [5, 5], 4: [0, 0]}, initial_health={1: 1.0, 2: 0.25}),
+    # the headline configuration (32x32, 64 agents, 2 teams), past one horizon
+    dict(name='tb_32', rows=32, cols=32, n_agents=64, n_teams=2, n_envs=2, n_steps=230,
+         horizon=200, seed_base=1000003),
+    # the reference example's layout: 24 agents, 4 teams on 4 corner cells
+    dict(name='tb_corners', rows=8, cols=8, n_agents=24, n_teams=4, n_envs=3, n_steps=80,
+         horizon=60, seed_base=5, corners=True),
+]
+
+DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
+                     view_range=3)
+
+
+def full_case(case):
+    c = dict(case)
+    nt = c['n_teams']
+    c.setdefault('overlap', {t: [t] for t in range(1, nt + 1)})
+    c.setdefault('attack_mapping', {t: [u for u in range(1, nt + 1) if u != t]
+                                    for t in range(1, nt + 1)})
+    c.setdefault('observe_self', True)
+    c.setdefault('no_overlap_at_reset', False)
+    c.setdefault('stacked_attacks', False)
+    c.setdefault('state_order', 'position_health')
+    c.setdefault('initial_positions', {})
+    c.setdefault('initial_health', {})
+    c.setdefault('agent', DEFAULT_AGENT)
+    if c.pop('corners', False):
+        corners = [[1, 1], [1, 6], [6, 1], [6, 6]]
+        c['initial_positions'] = {i: corners[i % 4] for i in range(c['n_agents'])}
+    c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
+    c['action_seed'] = 1234 + c['seed_base']
+    # json keys must be str
+    for k in ('overlap', 'attack_mapping', 'initial_positions', 'initial_health'):
+        c[k] = {str(kk): v for kk, v in c[k].items()}
+    return c
+
+
+def make_actions(c):
+    rng = np.random.RandomState(c['action_seed'])
+    T, E, A = c['n_steps'], c['n_envs'], c['n_agents']
+    mr = c['agent']['move_range']
+    act = np.zeros((T, E, A, 3), dtype=np.int8)
+    act[..., 0:2] = rng.randint(-mr, mr + 1, size=(T, E, A, 2))
+    act[..., 2] = rng.randint(0, 2, size=(T, E, A))
+    return act
+
+
+def build_reference_env(c):
+    from abmarl.examples.sim.team_battle_example import TeamBattleSim
+    from abmarl.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent, \
+        HealthAgent
+    from abmarl.sim.gridworld.state import PositionState, HealthState
+    from abmarl.managers import AllStepManager
+
+    class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
+        pass
+
+    agents = {}
+    for i in range(c['n_agents']):
+        kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])
+        if str(i) in c['initial_positions']:
+            kw['initial_position'] = np.array(c['initial_positions'][str(i)])
+        if str(i) in c['initial_health']:
+            kw['initial_health'] = c['initial_health'][str(i)]
+        agents[kw['id']] = Fighter(**kw)
+    sim = TeamBattleSim.build_sim(
+        c['rows'], c['cols'], agents=agents,
+        overlapping={int(k): set(v) for k, v in c['overlap'].items()},
+        attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
+        stacked_attacks=c['stacked_attacks'],
+        observe_self=c['observe_self'],
+        no_overlap_at_reset=c['no_overlap_at_reset'],
+        states={'PositionState', 'HealthState'},
+        observers={'PositionCenteredEncodingObserver'},
+        dones={'OneTeamRemainingDone'})
+    # pin the set-ordered state components (smart.py:37)
+    pos = [s for s in sim._states if isinstance(s, PositionState)][0]
+    hea = [s for s in sim._states if isinstance(s, HealthState)][0]
+    sim._states = [pos, hea] if c['state_order'] == 'position_health' else [hea, pos]
+    return AllStepManager(sim)
+
+
+def run_case(case):
+    c = full_case(case)
+    T, E, A = c['n_steps'], c['n_envs'], c['n_agents']
+    S = 2 * c['agent']['view_range'] + 1
+    act = make_actions(c)
+    ids = [f'agent{i}' for i in range(A)]
+
+    def obs_array(obs_dict):
+        out = np.full((A, S, S), -2, dtype=np.int8)
+        ret = np.zeros(A, dtype=np.uint8)
+        for i, aid in enumerate(ids):
+            if aid in obs_dict:
+                out[i] = obs_dict[aid]['position_centered_encoding']
+                ret[i] = 1
+        return out, ret
+
+    managers = [build_reference_env(c) for _ in range(E)]
+    rng_states = []
+    obs0 = np.zeros((E, A, S, S), dtype=np.int8)
+    for e in range(E):
+        np.random.seed(c['seeds'][e])
+        o = managers[e].reset()
+        obs0[e], _ = obs_array(o)
+        rng_states.append(np.random.get_state())
+
+    out = dict(
+        obs=np.zeros((T, E, A, S, S), dtype=np.int8),
+        returned=np.zeros((T, E, A), dtype=np.uint8),
+        reward=np.zeros((T, E, A), dtype=np.float64),
+        done=np.ones((T, E, A), dtype=np.uint8),
+        all_done=np.zeros((T, E), dtype=np.uint8),
+        pos=np.zeros((T, E, A, 2), dtype=np.int8),
+        health=np.zeros((T, E, A), dtype=np.float64),
+        active=np.zeros((T, E, A), dtype=np.uint8),
+        mt_pos=np.zeros((T, E), dtype=np.int16),
+        mt_crc=np.zeros((T, E), dtype=np.uint32),
+        reset_mask=np.zeros((T, E), dtype=np.uint8),
+        reset_obs=np.full((T, E, A, S, S), -2, dtype=np.int8),
+    )
+    steps = [0] * E
+    for t in range(T):
+        for e in range(E):
+            m = managers[e]
+            np.random.set_state(rng_states[e])
+            adict = {}
+            for i, aid in enumerate(ids):
+                if aid not in m.done_agents:
+                    adict[aid] = {'move': act[t, e, i, :2].astype(int), 'attack': int(act[t, e, i, 2])}
+            o, r, d, _ = m.step(adict)
+            steps[e] += 1
+            out['obs'][t, e], out['returned'][t, e] = obs_array(o)
+            for i, aid in enumerate(ids):
+                if aid in r:
+                    out['reward'][t, e, i] = r[aid]
+                    out['done'][t, e, i] = int(bool(d[aid]))
+                agent = m.agents[aid]
+                out['pos'][t, e, i] = agent.position
+                out['health'][t, e, i] = agent.health
+                out['active'][t, e, i] = int(agent.active)
+            out['all_done'][t, e] = int(bool(d['__all__']))
+            st = np.random.get_state()
+            out['mt_pos'][t, e] = st[2]
+            out['mt_crc'][t, e] = zlib.crc32(np.ascontiguousarray(st[1], dtype=np.uint32).tobytes())
+            if d['__all__'] or steps[e] >= c['horizon']:
+                ro = m.reset()
+                steps[e] = 0
+                out['reset_mask'][t, e] = 1
+                out['reset_obs'][t, e], _ = obs_array(ro)
+            rng_states[e] = np.random.get_state()
+    path = os.path.join(HERE, c['name'] + '.npz')
+    np.savez_compressed(path, case=json.dumps(c), actions=act, obs0=obs0, **out)
+    print(f"{c['name']}: {T} steps x {E} envs x {A} agents, resets={int(out['reset_mask'].sum())}, "
+          f"kills={int((out['reward'] > 0.5).sum())} -> {os.path.getsize(path)} B")
+
+
+def main():
+    sys.path.insert(0, HERE)
+    import gym_stub
+    gym_stub.install()
+    sys.path.insert(0, REF)
+    for case in CASES:
+        run_case(case)
+
+
+if __name__ == '__main__':
+    main()

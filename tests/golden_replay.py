@@ -1,0 +1,48 @@
+"""Replay a golden fixture through a runner and compare bit-exactly."""
+import zlib
+
+import numpy as np
+
+
+def _bits(x):
+    return np.ascontiguousarray(x, dtype=np.float64).view(np.uint64)
+
+
+def check_step(g, t, obs, rew, done, all_done, state=None, where=''):
+    E = g['all_done'].shape[1]
+    ok_obs = obs.astype(np.int64) == g['obs'][t].astype(np.int64)
+    assert ok_obs.all(), f"{where} step {t}: obs mismatch at {np.argwhere(~ok_obs)[:5].tolist()}"
+    bad = _bits(rew) != _bits(g['reward'][t])
+    assert not bad.any(), (f"{where} step {t}: reward mismatch at {np.argwhere(bad)[:5].tolist()}: "
+                           f"{rew[bad][:5]} vs {g['reward'][t][bad][:5]}")
+    assert (done == g['done'][t]).all(), f"{where} step {t}: done mismatch"
+    assert (all_done == g['all_done'][t]).all(), f"{where} step {t}: __all__ mismatch"
+    if state is not None:
+        assert (state['pos'] == g['pos'][t]).all(), f"{where} step {t}: positions differ"
+        h = state['health']
+        assert (h == g['health'][t]).all(), f"{where} step {t}: health differs"
+        act = (state['flags'] >> 2) & 1
+        assert (act == g['active'][t]).all(), f"{where} step {t}: active differs"
+        mt = state['mt']
+        for e in range(E):
+            assert int(mt[e, 624]) == int(g['mt_pos'][t, e]), f"{where} step {t} env {e}: RNG pos"
+            crc = zlib.crc32(np.ascontiguousarray(mt[e, :624], dtype=np.uint32).tobytes())
+            assert crc == int(g['mt_crc'][t, e]), f"{where} step {t} env {e}: RNG key digest"
+
+
+def replay(runner, g, with_state=True, steps=None):
+    """runner API: reset(mask=None) -> obs (E,A,S,S); step(actions) -> (obs, rew, done, all_done);
+    state() -> dict(pos, health, flags, mt)."""
+    obs0 = runner.reset(None)
+    assert (obs0 == g['obs0']).all(), "initial reset obs mismatch"
+    T = g['actions'].shape[0] if steps is None else steps
+    for t in range(T):
+        obs, rew, done, all_done = runner.step(g['actions'][t].astype(np.int32))
+        st = runner.state() if with_state else None
+        check_step(g, t, obs, rew, done, all_done, st, where=type(runner).__name__)
+        m = g['reset_mask'][t].astype(np.uint8)
+        if m.any():
+            robs = runner.reset(m)
+            sel = m.astype(bool)
+            assert (robs[sel] == g['reset_obs'][t][sel]).all(), f"step {t}: reset obs mismatch"
+    return T

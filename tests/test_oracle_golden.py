@@ -1,0 +1,39 @@
+"""The C oracle reproduces the reference's own trajectories bit-exactly
+(fixtures generated from /root/reference by tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from tests.cases import GOLDEN_CASES, load_golden, golden_config
+from tests.golden_replay import replay
+
+
+class OracleRunner:
+    def __init__(self, oracle_mod, g):
+        self.cc = golden_config(g)
+        c = g['case']
+        self.o = oracle_mod.Oracle(self.cc, c['n_envs'])
+        self.o.seed(c['seeds'])
+        self.obs = self.o.new_obs()
+        E, A = self.o.E, self.o.A
+        self.rew = np.zeros((E, A), np.float64)
+        self.done = np.zeros((E, A), np.uint8)
+        self.all_done = np.zeros(E, np.uint8)
+
+    def reset(self, mask):
+        err = self.o.reset(self.obs, mask=mask)
+        assert not err.any()
+        return self.obs.copy()
+
+    def step(self, actions):
+        self.o.step(actions, self.obs, self.rew, self.done, self.all_done)
+        return self.obs, self.rew, self.done, self.all_done
+
+    def state(self):
+        return self.o.state()
+
+
+@pytest.mark.parametrize('name', GOLDEN_CASES)
+def test_oracle_matches_reference(oracle_mod, name):
+    g = load_golden(name)
+    n = replay(OracleRunner(oracle_mod, g), g)
+    assert n == g['actions'].shape[0]
