@@ -23,7 +23,7 @@ SIGNATURES = {
     'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_set_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    'gw_random_actions': (_i32, [_vp, _u64, _u32, _vp, _vp]),
+    'gw_random_actions': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp]),
     'gw_destroy': (_i32, [_vp]),
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),

@@ -799,13 +799,13 @@ __device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
 }
 
 __global__ void random_actions_kernel(const DevAgent* spec, int E, int A, uint64_t key,
-                                      uint32_t step, int32_t* actions)
+                                      uint32_t step, uint32_t env_offset, int32_t* actions)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E * A) return;
     const int e = i / A, a = i % A;
     const DevAgent s = spec[a];
-    uint4 r = philox(make_uint4((uint32_t)e, step, (uint32_t)a, 0x5EED),
+    uint4 r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED),
                      make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
     const int m = s.move_range;
     const uint32_t span = (uint32_t)(2 * m + 1);
@@ -989,8 +989,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
 gw_status gw_destroy(gw_handle g)
 {
     if (!g) return GW_E_INVALID;
-    hipFree(g->base.pos); hipFree(g->base.health); hipFree(g->base.flags); hipFree(g->base.seq);
-    hipFree(g->base.mt); hipFree(g->base.steps); hipFree(g->d_spec);
+    (void)hipFree(g->base.pos); (void)hipFree(g->base.health); (void)hipFree(g->base.flags);
+    (void)hipFree(g->base.seq); (void)hipFree(g->base.mt); (void)hipFree(g->base.steps);
+    (void)hipFree(g->d_spec);
     delete g;
     return GW_OK;
 }
@@ -1058,12 +1059,13 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     return GW_OK;
 }
 
-gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, int32_t* actions, void* stream)
+gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t env_offset,
+                            int32_t* actions, void* stream)
 {
     if (!g || !actions) return GW_E_INVALID;
     const int n = g->E * g->A;
     hipLaunchKernelGGL(random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, actions);
+                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, env_offset, actions);
     HIPCHK(hipGetLastError());
     return GW_OK;
 }

@@ -91,13 +91,14 @@ class GridWorldEngine:
                                          _stream()), 'gw_step')
         return self.obs, self.reward, self.done, self.all_done
 
-    def random_actions(self, key, step, out=None):
-        """Synthetic random policy (Philox, keyed by key/env/step/agent)."""
+    def random_actions(self, key, step, env_offset=0, out=None):
+        """Synthetic random policy (Philox, keyed by key / global env / step / agent)."""
         out = self.actions if out is None else out
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_random_actions(self.h, int(key) & 0xFFFFFFFFFFFFFFFF,
-                                                   int(step) & 0xFFFFFFFF, _ptr(out), _stream()),
-                          'gw_random_actions')
+                                                   int(step) & 0xFFFFFFFF,
+                                                   int(env_offset) & 0xFFFFFFFF, _ptr(out),
+                                                   _stream()), 'gw_random_actions')
         return out
 
     def check_errors(self):

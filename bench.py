@@ -1,0 +1,204 @@
+"""Benchmark: agent-steps/s of random-policy TeamBattle rollouts on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): TeamBattle 32x32,
+64 BattleAgents in 2 teams, 4096 envs per GPU (weak scaling: N GPUs run
+N x 4096 envs, sharded by global env id, no data-path collective), horizon
+200 with on-device auto-reset.  One timed "step" = random-policy actions
+(Philox kernel) + the fused AllStepManager.step kernel + the masked
+auto-reset kernel, for every env.
+
+Metric: agent-steps/s = sum over env-steps of the acting (not-done) agents,
+the reference's len(action_dict), over all ranks / the max
+wall time over ranks.  The engine counts acting agents on device.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, 'BASELINE.json')))['metric']
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def team_battle_sim(rows=32, cols=32, n_agents=64, n_teams=2):
+    from abmarl_amd.examples import BattleAgent, TeamBattleSim
+    agents = {f'agent{i}': BattleAgent(id=f'agent{i}', encoding=i % n_teams + 1)
+              for i in range(n_agents)}
+    return TeamBattleSim.build_sim(
+        rows, cols, agents=agents,
+        overlapping={t: {t} for t in range(1, n_teams + 1)},
+        attack_mapping={t: {u for u in range(1, n_teams + 1) if u != t}
+                        for t in range(1, n_teams + 1)},
+        states={'PositionState', 'HealthState'},
+        observers={'PositionCenteredEncodingObserver'},
+        dones={'OneTeamRemainingDone'})
+
+
+def step_bytes(E, A, S):
+    """Algorithmic HBM bytes of one step launch:
+    per entity slot: actions 12 + obs 4*S*S + reward 8 + done 1 +
+    state read+write 2*(pos 8 + seq 4 + health 8 + flags 1); per env:
+    __all__ 1 + steps 2*4 + acting 2*8 + RNG pos/counter 2*8."""
+    per_slot = 12 + 4 * S * S + 8 + 1 + 2 * (8 + 4 + 8 + 1)
+    per_env = 1 + 8 + 16 + 16
+    return E * (A * per_slot + per_env)
+
+
+def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200):
+    """The oracle (C port of the reference step, OpenMP over envs) on this
+    host's cores, bounded to ~`seconds` of work on a sample of the workload."""
+    from oracle.oracle import Oracle, lib
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
+    lib().gwo_set_threads(threads)
+    o = Oracle(cc, envs)
+    from abmarl_amd.engine import env_seeds
+    o.seed(env_seeds(envs))
+    E, A, S = envs, cc.n_agents, cc.obs_side
+    obs = o.new_obs()
+    rew = np.zeros((E, A)); done = np.zeros((E, A), np.uint8); ad = np.zeros(E, np.uint8)
+    acting = np.zeros(E, np.uint64)
+    o.reset(obs)
+    rng = np.random.RandomState(7)
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < seconds:
+        act = np.zeros((E, A, 3), np.int32)
+        act[..., :2] = rng.randint(-1, 2, size=(E, A, 2))
+        act[..., 2] = rng.randint(0, 2, size=(E, A))
+        o.step(act, obs, rew, done, ad, acting)
+        o.reset(obs, all_done=ad, horizon=horizon)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return dict(value=float(acting.sum()) / dt, unit='agent-steps/s', cores=threads, kind='port',
+                sample=f'{envs} envs x {steps} steps (incl. action generation in numpy), '
+                       f'{dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--warmup', type=int, default=50)
+    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    ap.add_argument('--horizon', type=int, default=200)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    from abmarl_amd.parallel import shard_envs, gather_episode_stats
+    sim = team_battle_sim()
+    cc = sim.compiled()
+    E_local = args.envs
+    first, E_local = shard_envs(E_local * world, rank, world)
+    eng = GridWorldEngine(cc, E_local, seeds=env_seeds(E_local, run=0, first_env=first))
+    A, S = cc.n_agents, cc.obs_side
+    eng.reset()
+    torch.cuda.synchronize()
+    eng.check_errors()
+
+    key = 0x5eed0000  # policy key shared by all ranks; global env ids make streams distinct
+
+    def one_step(t, ev=None):
+        eng.random_actions(key, t, env_offset=first)
+        if ev is not None:
+            ev[0].record()
+        eng.step()
+        if ev is not None:
+            ev[1].record()
+        eng.reset(all_done=eng.all_done, horizon=args.horizon)
+
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
+    eng.check_errors()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    acting0 = int(eng.acting.sum().item())
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        one_step(args.warmup + t, evs[t])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    acting = int(eng.acting.sum().item()) - acting0
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
+    if dist:
+        acts = tot.clone(); dist.all_reduce(acts, op=dist.ReduceOp.SUM)
+        tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        kmax = torch.tensor([step_ms], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(kmax, op=dist.ReduceOp.MAX)
+        acting_all, dt_all, envs_all, step_ms_all = acts[0].item(), tmax[1].item(), acts[2].item(), kmax[0].item()
+    else:
+        acting_all, dt_all, envs_all, step_ms_all = acting, dt, E_local, step_ms
+    stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
+
+    if rank == 0:
+        value = acting_all / dt_all
+        nbytes = step_bytes(E_local, A, S)
+        achieved = nbytes / (step_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, 'profiles', 'pmc_step_kernel.json')
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+        out = {
+            'metric': METRIC,
+            'value': round(value, 1),
+            'unit': 'agent-steps/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(dt_all / args.steps * 1e3, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'int32 (positions/obs), f64 (health/reward)',
+            'data': 'synthetic: Philox random-policy actions, random-init TeamBattle episodes',
+            'config': {'workload': 'TeamBattle 32x32, 64 agents / 2 teams, 4096 envs per GPU, '
+                                   'horizon 200, auto-reset',
+                       'envs_per_gpu': E_local, 'global_envs': int(envs_all),
+                       'parallelism': f'env-sharded x{world} (no data-path collective)'},
+            'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
+            'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
+                         'traffic': traffic, 'kernel': 'step_kernel<7>',
+                         'kernel_ms': round(step_ms_all, 4),
+                         'bytes_per_launch': nbytes},
+            'episode_stats': stats,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

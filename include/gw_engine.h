@@ -169,10 +169,11 @@ gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
 
 /* Philox-4x32-10 random policy (uniform over MoveActor Box(-r,r,(2,)) and
    BinaryAttackActor Discrete(k+1)): actions for every entity of every env,
-   keyed by (key, env, step, agent).  Not part of the reference; it is the
-   benchmark's synthetic policy.                                              */
-gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, int32_t* actions,
-                            void* stream);
+   keyed by (key, env_offset + env, step, agent) so that a sharded run draws
+   the same actions for a global env id on any number of GPUs.  Not part of
+   the reference; it is the benchmark's synthetic policy.                     */
+gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
+                            int32_t* actions, void* stream);
 
 gw_status gw_destroy(gw_handle h);
 
