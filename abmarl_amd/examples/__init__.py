@@ -1,1 +1,2 @@
 from abmarl_amd.examples.team_battle import BattleAgent, TeamBattleSim  # noqa: F401
+from abmarl_amd.examples.multi_corridor import MultiCorridor  # noqa: F401

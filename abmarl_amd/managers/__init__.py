@@ -1,0 +1,2 @@
+from abmarl_amd.managers.simulation_manager import SimulationManager  # noqa: F401
+from abmarl_amd.managers.all_step_manager import AllStepManager  # noqa: F401

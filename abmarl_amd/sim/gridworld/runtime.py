@@ -1,0 +1,117 @@
+"""Dict-API runtime: one SmartGridWorldSimulation on a one-env engine.
+
+Every reset/step:
+  1. uploads the global numpy legacy RNG state (np.random.get_state()) into
+     the env's MT19937 slot,
+  2. runs the fused HIP reset / step,
+  3. reads the RNG state back into np.random (np.random.set_state), and
+     mirrors positions / health / active onto the agent objects.
+So ``np.random.seed(s); manager.reset(); manager.step(...)`` consumes and
+produces exactly what the reference does for the same seed.
+"""
+import numpy as np
+import torch
+
+from abmarl_amd import _abi
+from abmarl_amd.engine import GridWorldEngine
+from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent
+
+
+class DictRuntime:
+    def __init__(self, sim, compiled, device=None):
+        self.sim = sim
+        self.cc = compiled
+        self.ids = list(sim.agents.keys())
+        self.index = {aid: i for i, aid in enumerate(self.ids)}
+        self.eng = GridWorldEngine(compiled, 1, device=device, seeds=[0])
+        self.dev = self.eng.device
+        A = len(self.ids)
+        self.obs = np.full((A, self.cc.obs_side, self.cc.obs_side), -2, np.int32)
+        self.reward = np.zeros(A)
+        self.done = np.ones(A, np.uint8)
+        self.all_done = False
+        self.live = np.zeros(A, bool)
+        self.key = 'position_centered_encoding'
+        self.observes = [isinstance(a, GridObservingAgent) for a in sim.agents.values()]
+        self.sides = [2 * a.view_range + 1 if isinstance(a, GridObservingAgent) else 0
+                      for a in sim.agents.values()]
+
+    # -------------------------------------------------------------- RNG sync
+    def _push_rng(self):
+        st = np.random.get_state()
+        assert st[0] == 'MT19937'
+        mt = self.eng.get_state()['mt']
+        host = mt.cpu().numpy().view(np.uint32).copy()
+        host[0, :624] = st[1]
+        host[0, 624] = st[2]
+        self._gauss = st[3:]
+        self.eng.set_state(mt=torch.as_tensor(host.view(np.int32), device=self.dev))
+
+    def _pull(self):
+        st = self.eng.get_state()
+        torch.cuda.synchronize(self.dev)
+        host = {k: v.cpu().numpy() for k, v in st.items()}
+        mt = host['mt'].view(np.uint32)[0]
+        np.random.set_state(('MT19937', mt[:624].copy(), int(mt[624])) + tuple(self._gauss))
+        flags = host['flags'][0]
+        self.live = (flags & _abi.FLAG_LIVE) != 0
+        for i, agent in enumerate(self.sim.agents.values()):
+            agent.position = host['pos'][0, i].astype(int)
+            if isinstance(agent, HealthAgent):
+                agent._health = float(host['health'][0, i])
+            agent._active = bool(flags[i] & _abi.FLAG_ACTIVE)
+
+    # -------------------------------------------------------------- protocol
+    def reset(self):
+        self._push_rng()
+        obs = self.eng.reset()
+        self.eng.check_errors()
+        self.obs = obs[0].cpu().numpy()
+        self.reward[:] = 0
+        self.done[:] = 0
+        self.all_done = False
+        self._pull()
+
+    def step(self, action_dict):
+        ids = [a for a in action_dict]
+        order = [self.index[a] for a in ids]
+        if order != sorted(order):
+            raise NotImplementedError(
+                "the engine processes actions in agents-dict order; got a different order")
+        act = np.zeros((1, len(self.ids), _abi.GW_ACT_DIM), np.int32)
+        act[0, :, 2] = -1                      # not in action_dict: does not act
+        for aid, a in action_dict.items():
+            i = self.index[aid]
+            assert self.live[i], "Received an action for an agent that is already done."
+            mv = a.get('move', (0, 0)) if isinstance(a, dict) else (0, 0)
+            act[0, i, 0:2] = np.asarray(mv, dtype=np.int64)
+            act[0, i, 2] = int(a.get('attack', 0)) if isinstance(a, dict) else 0
+        self._push_rng()
+        obs, rew, done, all_done = self.eng.step(torch.as_tensor(act, device=self.dev))
+        self.obs = obs[0].cpu().numpy()
+        self.reward = rew[0].cpu().numpy().copy()
+        self.done = done[0].cpu().numpy().copy()
+        self.all_done = bool(all_done[0].item())
+        self._pull()
+
+    def get_obs(self, agent_id):
+        i = self.index[agent_id]
+        if not self.observes[i]:
+            return {}
+        s = self.sides[i]
+        return {self.key: self.obs[i, :s, :s].astype(int)}
+
+    def get_reward(self, agent_id):
+        i = self.index[agent_id]
+        r = float(self.reward[i])
+        self.reward[i] = 0.0
+        return r
+
+    def get_done(self, agent_id):
+        return bool(self.done[self.index[agent_id]])
+
+    def get_all_done(self):
+        return self.all_done
+
+    def done_agents(self):
+        return {aid for aid, lv in zip(self.ids, self.live) if not lv}

@@ -199,6 +199,35 @@ def run_case(case):
           f"kills={int((out['reward'] > 0.5).sum())} -> {os.path.getsize(path)} B")
 
 
+def run_multicorridor(randomize=False, n_steps=60):
+    """BASELINE config 1: MultiCorridor + AllStepManager, np.random.seed(24)
+    (tests/test_all_step_multi_corridor.py), scripted random actions."""
+    import random
+    from abmarl.examples import MultiCorridor
+    from abmarl.managers import AllStepManager
+    rng = np.random.RandomState(99)
+    np.random.seed(24)
+    random.seed(24)
+    sim = AllStepManager(MultiCorridor(), randomize_action_input=randomize)
+
+    def enc(d):
+        return {k: {kk: np.asarray(vv).tolist() for kk, vv in v.items()} for k, v in d.items()}
+
+    records = [{'reset': enc(sim.reset())}]
+    for t in range(n_steps):
+        acts = {aid: int(rng.randint(0, 3)) for aid in sim.agents if aid not in sim.done_agents}
+        o, r, d, _ = sim.step(acts)
+        rec = {'actions': acts, 'obs': enc(o), 'reward': {k: float(v) for k, v in r.items()},
+               'done': {k: bool(v) for k, v in d.items()}}
+        if d['__all__']:
+            rec['reset'] = enc(sim.reset())
+        records.append(rec)
+    name = 'multicorridor_shuffled' if randomize else 'multicorridor'
+    path = os.path.join(HERE, name + '.json')
+    json.dump(records, open(path, 'w'))
+    print(f"{name}: {n_steps} steps -> {os.path.getsize(path)} B")
+
+
 def main():
     sys.path.insert(0, HERE)
     import gym_stub
@@ -206,6 +235,8 @@ def main():
     sys.path.insert(0, REF)
     for case in CASES:
         run_case(case)
+    run_multicorridor(False)
+    run_multicorridor(True)
 
 
 if __name__ == '__main__':

@@ -1,0 +1,73 @@
+"""Drop-in check at the reference's own API level on the GPU:
+np.random.seed(s) + AllStepManager(TeamBattleSim...) reset/step dicts match
+the reference's trajectories (golden fixtures) exactly, and the global
+np.random stream ends in the same state (position + key digest)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from abmarl_amd.managers import AllStepManager
+from abmarl_amd.external import MultiAgentWrapper
+from tests.cases import GOLDEN_CASES, load_golden, build_sim
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_obs(d, ref, returned):
+    ids = sorted(d, key=lambda k: int(k[5:]))
+    assert [int(k[5:]) for k in ids] == list(np.nonzero(returned)[0])
+    for k in ids:
+        got = d[k]['position_centered_encoding']
+        np.testing.assert_array_equal(got, ref[int(k[5:])])
+
+
+@pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners'])
+def test_dict_api_matches_reference(name):
+    g = load_golden(name)
+    c = g['case']
+    A = c['n_agents']
+    for e in range(min(3, c['n_envs'])):
+        sim = build_sim(c)
+        env = MultiAgentWrapper(AllStepManager(sim))
+        np.random.seed(c['seeds'][e])
+        obs = env.reset()
+        _check_obs(obs, g['obs0'][e], np.ones(A))
+        for t in range(g['actions'].shape[0]):
+            done_agents = env.sim.done_agents
+            adict = {f'agent{i}': {'move': g['actions'][t, e, i, :2].astype(int),
+                                   'attack': int(g['actions'][t, e, i, 2])}
+                     for i in range(A) if f'agent{i}' not in done_agents}
+            o, r, d, _ = env.step(adict)
+            _check_obs(o, g['obs'][t, e], g['returned'][t, e])
+            for k, v in r.items():
+                i = int(k[5:])
+                assert np.float64(v).view(np.uint64) == g['reward'][t, e, i].view(np.uint64), \
+                    (t, k, v, g['reward'][t, e, i])
+                assert bool(d[k]) == bool(g['done'][t, e, i])
+            assert bool(d['__all__']) == bool(g['all_done'][t, e])
+            st = np.random.get_state()
+            assert st[2] == g['mt_pos'][t, e]
+            assert zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes()) == g['mt_crc'][t, e]
+            for i, agent in enumerate(sim.agents.values()):
+                np.testing.assert_array_equal(agent.position, g['pos'][t, e, i])
+                assert agent.health == g['health'][t, e, i]
+            if g['reset_mask'][t, e]:
+                ro = env.reset()
+                _check_obs(ro, g['reset_obs'][t, e], np.ones(A))
+
+
+def test_batched_env_autoreset_runs():
+    import torch
+    from abmarl_amd.external import BatchedMultiAgentEnv
+    from tests.cases import team_battle  # noqa: F401
+    g = load_golden('tb_small')
+    sim = build_sim(g['case'])
+    env = BatchedMultiAgentEnv(sim, 32, horizon=20)
+    env.reset()
+    for t in range(60):
+        a = env.engine.random_actions(123, t)
+        obs, rew, done, ad = env.step(a)
+    torch.cuda.synchronize()
+    assert obs.shape == (32, 8, 7, 7)
+    assert int(env.engine.get_state()['steps'].max()) <= 20
