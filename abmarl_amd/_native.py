@@ -11,6 +11,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(PKG, 'csrc', 'gw_engine.hip')
 INCLUDE = os.path.join(os.path.dirname(PKG), 'include', 'gw_engine.h')
 LIB = os.path.join(PKG, '_build', 'libgw_engine.so')
+# diagnostic build with in-kernel s_memtime stamps (tools/stamps.py); never the default
+LIB_STAMPS = os.path.join(PKG, '_build', 'libgw_engine_stamps.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('GW_OFFLOAD_ARCH', 'gfx950')
 
@@ -21,6 +23,7 @@ SIGNATURES = {
     'gw_seed': (_i32, [_vp, _vp, _vp]),
     'gw_reset': (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_step_autoreset': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_set_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_random_actions': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp]),
@@ -32,20 +35,22 @@ SIGNATURES = {
 }
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, stamps=False):
     """Compile the engine for gfx950 with hipcc (works without a GPU)."""
+    out = LIB_STAMPS if stamps else LIB
     deps = [SRC, INCLUDE]
-    if not force and os.path.exists(LIB) and \
-            os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
-        return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    if not force and os.path.exists(out) and \
+            os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off',
-           '-fPIC', '-shared', '-Wno-unused-result', '-o', LIB + '.tmp', SRC]
+           '-fPIC', '-shared', '-Wno-unused-result'] + (['-DGW_STAMPS'] if stamps else []) + \
+        ['-o', out + '.tmp', SRC]
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd)
-    os.replace(LIB + '.tmp', LIB)
-    return LIB
+    os.replace(out + '.tmp', out)
+    return out
 
 
 _lib = None
@@ -55,10 +60,11 @@ def lib():
     """The loaded engine library; raises if it is missing (no fallback)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
+        if not os.path.exists(LIB_STAMPS if os.environ.get('GW_ENGINE_STAMPS') == '1' else LIB):
             raise RuntimeError(f"HIP engine library {LIB} is missing; run "
                                "`python -c 'import __graft_entry__ as g; g.build()'`")
-        L = C.CDLL(LIB)
+        path = LIB_STAMPS if os.environ.get('GW_ENGINE_STAMPS') == '1' else LIB
+        L = C.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -3,28 +3,34 @@
 // Execution model: ONE WAVEFRONT PER ENVIRONMENT, one lane per entity
 // (A <= 64).  The reference's step is a sequence of Python loops over the
 // agents dict whose random draws come from one sequential MT19937 stream
-// (numpy legacy RandomState); everything that changes the RNG stream or the
-// grid in reference order is kept in reference order here, and everything
-// else is lane-parallel:
+// (numpy legacy RandomState).  Whatever changes the RNG stream or the grid in
+// reference order is kept in reference order here; everything else is
+// lane-parallel:
 //
-//   attack pass (team_battle_example.py:35-47 / actor.py:306-501)
-//       serial over attackers; each attacker's window scan is one ballot,
-//       candidates are extracted in (window cell, in-cell insertion order)
-//       with a wave min-reduction, accuracy draws / permutation draws are
-//       issued in reference order from a register-cached MT19937 block.
-//   move pass   (team_battle_example.py:50-55 / actor.py:82-114)
-//       serial over movers; Grid.query is one ballot over the lanes.
-//   observation (all_step_manager.py:68-71 / observer.py:204-250)
-//       lane-parallel window gather from an LDS occupancy table
-//       (count | xor-of-encodings per cell, rebuilt after the moves); the
-//       rare cells with >= 2 candidate occupants (np.random.choice draws) are
-//       resolved afterwards in (agent, row, col) order.
+//   attack pass (team_battle_example.py:35-47, actor.py:306-501)
+//       a lane-parallel pre-check on the LDS cell table finds the attackers
+//       whose window holds no possible target (they only take the -0.1);
+//       the others run serially in agent order: one ballot = the window scan,
+//       candidates ordered by (window cell, in-cell insertion order) with
+//       ballot ranks, accuracy / permutation draws in reference order.
+//   move pass   (team_battle_example.py:50-55, actor.py:82-114)
+//       movers whose source/target cells no other mover touches are resolved
+//       in parallel against the post-attack cell table; the rest run serially
+//       in agent order with Grid.query as one ballot.
+//   observation (all_step_manager.py:68-71, observer.py:204-250)
+//       lane-parallel: each window row is 2-3 LDS dword reads of a padded
+//       byte table (0 empty, enc single, 0x80 crowded, 0xFF off-grid); the
+//       rare crowded cells (np.random.choice draws) are resolved afterwards in
+//       (agent, row, col) order; int8 staging -> coalesced int32 stores.
 //   reward / done / __all__ (smart.py:101-117, done.py:39-56,140-153,
-//       all_step_manager.py:72-93): lane-parallel + ballots.
+//       all_step_manager.py:72-93): lane-parallel + ballots / DPP reductions.
+//   auto-reset (optional, same launch): AllStepManager.reset for the envs
+//       whose episode ended (PositionState / HealthState / observation).
 //
 // The grid's insertion-ordered dict cells are represented by a per-agent
 // placement sequence number (seq): the order of agents inside a cell is the
-// order of their seq.  No grid array lives in HBM.
+// order of their seq.  No grid array lives in HBM; LDS tables are rebuilt per
+// launch from the agents' positions.
 //
 // Data layout in HBM (SoA, env-major, lane-contiguous => coalesced):
 //   pos[E][A] int2, health[E][A] f64, flags[E][A] u8, seq[E][A] u32,
@@ -44,6 +50,8 @@
 #define MT_POS_SLOT 624
 #define MT_CTR_SLOT 625
 #define SEQ_RENORM (1u << 23)
+#define CELL_CROWD 0x80u
+#define CELL_OFF 0xFFu
 
 namespace {
 
@@ -63,11 +71,13 @@ struct Params {
     // I/O
     const int32_t* actions; int32_t* obs; double* reward; uint8_t* done; uint8_t* all_done;
     uint64_t* acting; uint32_t* err;
-    const uint8_t* mask; const uint8_t* prev_all_done; int32_t horizon;
+    const uint8_t* mask; const uint8_t* prev_all_done; int32_t horizon; int32_t autoreset;
+    uint64_t* stamps;   // diagnostic build only (-DGW_STAMPS): [E][16] s_memtime
     // config
     int32_t E, A, H, W, max_enc, sim_kind, nav, target;
     int32_t observe_self, stacked, no_overlap_at_reset, state_order;
     uint32_t done_kind;
+    int32_t pad, pitch, tbl_rows;          // padded byte table geometry
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
 };
@@ -89,6 +99,7 @@ __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_read
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ int32_t rl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ bool rlb(bool v, int l) { return __builtin_amdgcn_readlane((int)v, l) != 0; }
 
 __device__ __forceinline__ double rld(double v, int l)
 {
@@ -98,33 +109,65 @@ __device__ __forceinline__ double rld(double v, int l)
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+__device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
+
+// DPP (GFX9 row_shr / row_bcast) wave primitives; call in uniform control flow
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, WAVE));
-    return uni(v);
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v += dpp<0x111>(0u, v);          // row_shr:1
+    v += dpp<0x112>(0u, v);          // row_shr:2
+    v += dpp<0x114>(0u, v);          // row_shr:4
+    v += dpp<0x118>(0u, v);          // row_shr:8
+    v += dpp<0x142, 0xa>(0u, v);     // row_bcast:15 -> rows 1, 3
+    v += dpp<0x143, 0xc>(0u, v);     // row_bcast:31 -> rows 2, 3
+    return v;
 }
 
 __device__ __forceinline__ uint32_t wave_or(uint32_t v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, WAVE);
-    return uni(v);
+    v |= dpp<0x111>(0u, v);
+    v |= dpp<0x112>(0u, v);
+    v |= dpp<0x114>(0u, v);
+    v |= dpp<0x118>(0u, v);
+    v |= dpp<0x142, 0xa>(0u, v);
+    v |= dpp<0x143, 0xc>(0u, v);
+    return rl(v, WAVE - 1);
 }
 
-__device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
-
-// inclusive prefix sum over the wave
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+// k-th (0-based) set bit of w (k < popcount(w))
+__device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
 {
-    const int l = lane_id();
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        uint32_t t = (uint32_t)__shfl_up((int)v, off, WAVE);
-        if (l >= off) v += t;
-    }
-    return v;
+    int base = 0;
+    uint32_t lo = (uint32_t)w;
+    uint32_t pl = (uint32_t)__popc(lo);
+    uint32_t x = lo;
+    if (k >= pl) { k -= pl; x = (uint32_t)(w >> 32); base = 32; }
+    uint32_t p16 = (uint32_t)__popc(x & 0xffffu);
+    if (k >= p16) { k -= p16; x >>= 16; base += 16; }
+    uint32_t p8 = (uint32_t)__popc(x & 0xffu);
+    if (k >= p8) { k -= p8; x >>= 8; base += 8; }
+    for (uint32_t t = 0; t < k; t++) x &= x - 1;
+    return base + (int)__builtin_ctz(x);
 }
+
+// ------------------------------------------------------------ diagnostics
+#ifdef GW_STAMPS
+#define STAMP(i)                                                                  \
+    do {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        uint64_t _t = __builtin_amdgcn_s_memtime();                               \
+        if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * 16 + (i)] = _t;      \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+    } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
 
 // ------------------------------------------------------------ MT19937
 // numpy legacy RandomState (mt19937.c): key[] lives in LDS; tempered output
@@ -211,7 +254,7 @@ struct Lane {
     // constants
     int enc; uint32_t kind; int view, mrange, arange, simul;
     double strength, accuracy, init_health;
-    uint32_t ov;      // overlap mask of this lane's encoding
+    uint32_t ov, amap;   // overlap / attack masks of this lane's encoding
     int init_r, init_c;
     // state
     int r, c; uint32_t seq; double health; bool in_grid, live, active;
@@ -228,6 +271,7 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
         L.accuracy = s.accuracy; L.init_health = s.init_health; L.init_r = s.init_r;
         L.init_c = s.init_c;
         L.ov = p.overlap[s.enc];
+        L.amap = p.amap[s.enc];
         size_t k = (size_t)e * p.A + l;
         int2 q = p.pos[k];
         L.r = q.x; L.c = q.y;
@@ -238,6 +282,7 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
     } else {
         L.enc = 0; L.kind = 0; L.view = L.mrange = L.arange = L.simul = 0;
         L.strength = L.accuracy = L.init_health = 0; L.init_r = L.init_c = -1; L.ov = 0;
+        L.amap = 0;
         L.r = L.c = -1000; L.seq = 0; L.health = 0; L.in_grid = L.live = L.active = false;
     }
     L.reward = 0.0;
@@ -254,30 +299,68 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
 }
 
 // LDS carve-up per wave (dynamic shared memory, 16-B aligned pieces)
+//   key  [640] u32          MT19937 state
+//   tbl  [tbl_rows*pitch] u8 padded cell table: 0 empty, enc single,
+//                           0x80 >= 2 occupants, 0xFF off-grid (border)
+//   cnt  [ceil(HW/4)] u32   per-cell occupant counts, packed u8
+//   work union: { tcnt, scnt [2][ceil(HW/4)] u32 (move isolation)
+//               | stage [A*SS] i8 (observations)
+//               | avail [(max_enc+1)*64] u64 (reset availability bitmaps) }
 struct Smem {
-    uint32_t* key;     // [624]  (pad 640)
-    uint32_t* cell;    // [HW]   count | xor(enc) << 16
-    int8_t* stage;     // [A*SS] observation staging (pad to 16)
-    uint64_t* avail;   // [(max_enc+1) * 64] reset availability bitmaps
+    uint32_t* key;
+    uint8_t* tbl;
+    uint32_t* cnt;
+    uint32_t* tcnt;
+    uint32_t* scnt;
+    int8_t* stage;
+    uint64_t* avail;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, bool reset)
+__host__ __device__ inline size_t work_bytes(int HW, int A, int SS, int max_enc)
 {
-    size_t b = align16(GW_MT_STRIDE * 4) + align16((size_t)HW * 4) + align16((size_t)A * SS);
-    if (reset) b += align16((size_t)(max_enc + 1) * 64 * 8);
-    return b;
+    size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
+    size_t s = align16((size_t)A * SS);
+    size_t v = align16((size_t)(max_enc + 1) * 64 * 8);
+    if (s > w) w = s;
+    if (v > w) w = v;
+    return w;
 }
 
-__device__ __forceinline__ Smem carve(char* base, int HW, int A, int SS)
+__host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, int tbl_bytes)
 {
+    return align16(GW_MT_STRIDE * 4) + align16((size_t)tbl_bytes) +
+           align16((size_t)((HW + 3) / 4) * 4) + work_bytes(HW, A, SS, max_enc);
+}
+
+__device__ __forceinline__ Smem carve(char* base, const Params& p)
+{
+    const int HW = p.H * p.W;
     Smem s;
     s.key = (uint32_t*)base; base += align16(GW_MT_STRIDE * 4);
-    s.cell = (uint32_t*)base; base += align16((size_t)HW * 4);
-    s.stage = (int8_t*)base; base += align16((size_t)A * SS);
+    s.tbl = (uint8_t*)base; base += align16((size_t)p.tbl_rows * p.pitch);
+    s.cnt = (uint32_t*)base; base += align16((size_t)((HW + 3) / 4) * 4);
+    s.tcnt = (uint32_t*)base;
+    s.scnt = (uint32_t*)(base + align16((size_t)((HW + 3) / 4) * 4));
+    s.stage = (int8_t*)base;
     s.avail = (uint64_t*)base;
     return s;
+}
+
+__device__ __forceinline__ int tbl_idx(const Params& p, int r, int c)
+{
+    return (r + p.pad) * p.pitch + (c + p.pad);
+}
+
+__device__ __forceinline__ uint32_t cnt_get(const uint32_t* cnt, int cell)
+{
+    return (cnt[cell >> 2] >> (8 * (cell & 3))) & 0xffu;
+}
+
+__device__ __forceinline__ uint8_t cell_byte(uint32_t count, int enc)
+{
+    return count == 0 ? 0 : (count == 1 ? (uint8_t)enc : (uint8_t)CELL_CROWD);
 }
 
 __device__ __forceinline__ void load_rng(const Params& p, int e, Smem& sm, Rng& rng)
@@ -305,17 +388,50 @@ __device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, cons
     if (l == 0) { dst[MT_POS_SLOT] = (uint32_t)rng.pos; dst[MT_CTR_SLOT] = ctr; }
 }
 
-// rebuild the LDS occupancy table from the lanes (count | xor enc << 16)
-__device__ __forceinline__ void build_cells(const Params& p, Smem& sm, const Lane& L)
+// Build the padded byte table and the counts from the lanes' positions.
+__device__ void build_tables(const Params& p, Smem& sm, const Lane& L)
 {
+    const int l = lane_id();
     const int HW = p.H * p.W;
-    for (int i = lane_id(); i < HW; i += WAVE) sm.cell[i] = 0u;
-    wave_sync();
-    if (L.in_grid) {
-        int ci = L.r * p.W + L.c;
-        atomicAdd(&sm.cell[ci], 1u);
-        atomicXor(&sm.cell[ci], (uint32_t)L.enc << 16);
+    const int nw = (HW + 3) / 4;
+    // border = 0xFF, interior = 0 (pitch is a multiple of 4: a dword never spans rows)
+    const int tdw = p.tbl_rows * p.pitch / 4;
+    uint32_t* t32 = (uint32_t*)sm.tbl;
+    for (int i = l; i < tdw; i += WAVE) {
+        const int row = (i * 4) / p.pitch - p.pad;
+        const int col0 = (i * 4) % p.pitch - p.pad;
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int col = col0 + b;
+            const bool off = row < 0 || row >= p.H || col < 0 || col >= p.W;
+            w |= (off ? CELL_OFF : 0u) << (8 * b);
+        }
+        t32[i] = w;
     }
+    for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
+    wave_sync();
+    int cell = L.r * p.W + L.c;
+    if (L.in_grid) atomicAdd(&sm.cnt[cell >> 2], 1u << (8 * (cell & 3)));
+    wave_sync();
+    if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, cell), L.enc);
+    wave_sync();
+}
+
+// cell table update after agent b (uniform) left cell (r, c): count-1, new byte
+__device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const Lane& L, int b, int r, int c)
+{
+    const int l = lane_id();
+    const int cell = r * p.W + c;
+    if (l == b) atomicSub(&sm.cnt[cell >> 2], 1u << (8 * (cell & 3)));
+    wave_sync();
+    const uint32_t n = cnt_get(sm.cnt, cell);
+    int enc = 0;
+    if (n == 1) {
+        const uint64_t m = __ballot(L.in_grid && L.r == r && L.c == c);
+        enc = rl(L.enc, first_lane(m));
+    }
+    if (l == 0) sm.tbl[tbl_idx(p, r, c)] = cell_byte(n, enc);
     wave_sync();
 }
 
@@ -326,80 +442,89 @@ __device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const La
 {
     constexpr int SS = S * S;
     constexpr int R = S / 2;
-    constexpr int NW = (SS + 63) / 64;
+    constexpr int ND = (S + 3 + 3) / 4;       // dwords covering S bytes at any alignment
     const int l = lane_id();
     const int A = p.A;
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
-    uint64_t ev[NW];
-#pragma unroll
-    for (int w = 0; w < NW; w++) ev[w] = 0;
+    bool has_ev = false;
 
     if (l < A) {
         int8_t* st = sm.stage + l * SS;
-        for (int wr = 0; wr < S; wr++) {
-            const int gr = L.r - R + wr;
-            for (int wc = 0; wc < S; wc++) {
-                const int gc = L.c - R + wc;
-                const int k = wr * S + wc;
-                int v = -2;
-                if (obs_me) {
-                    if (gr < 0 || gr >= p.H || gc < 0 || gc >= p.W) v = -1;
-                    else {
-                        uint32_t w = sm.cell[gr * p.W + gc];
-                        int cnt = (int)(w & 0xffffu);
-                        int x = (int)(w >> 16);
-                        if (!p.observe_self && L.in_grid && gr == L.r && gc == L.c) { cnt -= 1; x ^= L.enc; }
-                        if (cnt == 0) v = 0;
-                        else if (cnt == 1) v = x;
-                        else { v = 0; ev[k >> 6] |= 1ull << (k & 63); }
+        if (obs_me) {
+            const uint32_t* t32 = (const uint32_t*)sm.tbl;
+            uint32_t rows[S][ND];
+            // every window row's dwords first (independent LDS reads), then decode
+            const int o0 = tbl_idx(p, L.r - R, L.c - R);
+#pragma unroll
+            for (int wr = 0; wr < S; wr++) {
+                const int o = o0 + wr * p.pitch;
+#pragma unroll
+                for (int d = 0; d < ND; d++) rows[wr][d] = t32[(o >> 2) + d];
+            }
+            const int sh = o0 & 3;
+#pragma unroll
+            for (int wr = 0; wr < S; wr++) {
+#pragma unroll
+                for (int d = 0; d + 1 < ND; d++) {
+                    const uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
+                    const uint32_t ev = w & 0x80808080u & ~(w << 1);
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const int wc = d * 4 + b;
+                        if (wc < S) {
+                            uint32_t v = (w >> (8 * b)) & 0xffu;
+                            if (wr == R && wc == R && !p.observe_self && L.in_grid && v != CELL_CROWD)
+                                v = 0;                      // alone on my cell, not observing myself
+                            st[wr * S + wc] = (int8_t)v;
+                            has_ev |= ((ev >> (8 * b)) & 0x80u) != 0;
+                        }
                     }
                 }
-                st[k] = (int8_t)v;
             }
+        } else {
+            for (int k = 0; k < SS; k++) st[k] = -2;
         }
     }
     wave_sync();
+    STAMP(8);
 
-    // serial: cells with >= 2 candidates draw np.random.choice in
-    // (agent, row, col) order (observer.py:224-246)
-    uint64_t any = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) any |= ev[w];
-    uint64_t olanes = __ballot(any != 0);
+    // serial: crowded cells draw np.random.choice in (agent, row, col) order
+    // (observer.py:224-246)
+    uint64_t olanes = __ballot(has_ev);
     while (olanes) {
         const int o = first_lane(olanes);
         olanes &= olanes - 1;
         const int orr = rl(L.r, o), oc = rl(L.c, o);
-#pragma unroll
-        for (int w = 0; w < NW; w++) {
-            uint32_t lo = rl((uint32_t)ev[w], o), hi = rl((uint32_t)(ev[w] >> 32), o);
-            uint64_t bits = ((uint64_t)hi << 32) | lo;
+        for (int k0 = 0; k0 < SS; k0 += WAVE) {
+            const int k = k0 + l;
+            const bool crowd = k < SS && (uint8_t)sm.stage[o * SS + k] == CELL_CROWD;
+            uint64_t bits = __ballot(crowd);
             while (bits) {
-                const int k = w * 64 + (int)__builtin_ctzll(bits);
+                const int kk = k0 + (int)__builtin_ctzll(bits);
                 bits &= bits - 1;
-                const int gr = orr - R + k / S, gc = oc - R + k % S;
+                const int gr = orr - R + kk / S, gc = oc - R + kk % S;
                 const bool mem = l < A && L.in_grid && L.r == gr && L.c == gc && (p.observe_self || l != o);
-                uint64_t mm = __ballot(mem);
+                const uint64_t mm = __ballot(mem);
                 const int n = __popcll(mm);
                 const uint32_t j = rng.interval((uint32_t)(n - 1));
                 // the j-th member in insertion (seq) order
-                uint32_t sel = 0;
-                for (uint32_t t = 0; t <= j; t++) {
-                    uint32_t key = (mem && ((mm >> l) & 1)) ? L.seq : 0xffffffffu;
-                    uint32_t mn = wave_min(key);
-                    uint64_t hit = __ballot(((mm >> l) & 1) && L.seq == mn);
-                    sel = first_lane(hit);
-                    mm &= ~(1ull << sel);
+                int sel = first_lane(mm);
+                for (uint64_t it = mm; it; it &= it - 1) {
+                    const int m = first_lane(it);
+                    const uint32_t sq = rl(L.seq, m);
+                    const uint32_t rank = (uint32_t)__popcll(__ballot(mem && L.seq < sq));
+                    if (rank == j) { sel = m; break; }
                 }
-                const int val = rl(L.enc, (int)sel);
-                if (l == 0) sm.stage[o * SS + k] = (int8_t)val;
+                const int val = rl(L.enc, sel);
+                if (l == 0) sm.stage[o * SS + kk] = (int8_t)val;
             }
         }
     }
     wave_sync();
+    STAMP(9);
 
     // stage (int8) -> obs (int32), 4 values per lane per iteration, coalesced
-    const int total = A * SS;                  // multiple of 4? handle tail
+    const int total = A * SS;
     int32_t* out = p.obs + (size_t)e * total;
     for (int i = l * 4; i < total; i += WAVE * 4) {
         if (i + 3 < total && (((size_t)e * total + i) & 3) == 0) {
@@ -414,44 +539,65 @@ __device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const La
 }
 
 // ------------------------------------------------------------ attack
+// Window scan of this lane's attack: could any agent be a candidate?
+// (superset test on the cell table; crowded cells count as possible)
+__device__ __forceinline__ bool attack_precheck(const Params& p, const Smem& sm, const Lane& L)
+{
+    const int R = L.arange;
+    bool any = false;
+    for (int dr = -R; dr <= R; dr++) {
+        for (int dc = -R; dc <= R; dc++) {
+            const uint32_t b = sm.tbl[tbl_idx(p, L.r + dr, L.c + dc)];
+            if (b == CELL_OFF || b == 0) continue;
+            if (dr == 0 && dc == 0 && b != CELL_CROWD) continue;   // just me
+            if (b == CELL_CROWD || ((L.amap >> b) & 1u)) any = true;
+        }
+    }
+    return any;
+}
+
 // BinaryAttackActor.process_action for attacker a with k attacks.
-// Returns status (attempted) and appends the attacked lanes (in list order)
-// to `list` (registers of lane t hold list[t]).  Applies damage.
-__device__ __forceinline__ bool attack_one(const Params& p, Rng& rng, Lane& L, int a, int k,
-                                           int& nlist, int& list)
+// Returns status (attempted); list (register of lane t) = attacked lanes in
+// list order; applies damage and updates the cell table for kills.
+__device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, Lane& L, int a,
+                                           int k, int& nlist, int& list)
 {
     const int l = lane_id();
     nlist = 0;
+    list = -1;
     const uint32_t akind = rl(L.kind, a);
     if (!(akind & GW_K_ATTACKING)) return false;
     if (k == 0) return false;
-    const int ar = rl(L.r, a), ac = rl(L.c, a), aenc = rl(L.enc, a);
+    const int ar = rl(L.r, a), ac = rl(L.c, a);
     const int R = rl(L.arange, a);
     const double acc = rld(L.accuracy, a);
-    const uint32_t amap = p.amap[aenc];
+    const uint32_t amap = rl(L.amap, a);
     const int D = 2 * R + 1;
     const int dr = L.r - ar, dc = L.c - ac;
     const bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
                       dr >= -R && dr <= R && dc >= -R && dc <= R;
-    const uint32_t ckey = cand ? ((uint32_t)((dr + R) * D + (dc + R)) << 24) | L.seq : 0xffffffffu;
-    uint64_t cm = __ballot(cand);
-    int rank = -1;
+    const uint32_t ckey = ((uint32_t)((dr + R) * D + (dc + R)) << 24) | L.seq;
+    const uint64_t cm = __ballot(cand);
+    // rank of every candidate in (window cell, insertion) order
+    int crank = -1;
+    for (uint64_t it = cm; it; it &= it - 1) {
+        const int j = first_lane(it);
+        const uint32_t kj = rl(ckey, j);
+        const int rk = __popcll(__ballot(cand && ckey < kj));
+        if (l == j) crank = rk;
+    }
+    const int ncand = __popcll(cm);
+    int rank = -1;                                         // rank among accepted
     int n = 0;
-    while (cm) {
-        int j;
-        if ((cm & (cm - 1)) == 0) j = first_lane(cm);
-        else {
-            uint32_t mn = wave_min(((cm >> l) & 1) ? ckey : 0xffffffffu);
-            j = first_lane(__ballot(((cm >> l) & 1) && ckey == mn));
-        }
-        cm &= ~(1ull << j);
+    for (int r = 0; r < ncand; r++) {
+        const int j = first_lane(__ballot(crank == r));
         const double u = rng.uniform();                     // _basic_criteria draw
         if (u > acc) continue;
         if (l == j) rank = n;
         n++;
     }
     if (n == 0) return true;                                // (True, [])
-    // _subset_attackables: list[t] (lane t) = accepted rank
+    // _subset_attackables: pick (lane t) = accepted rank of list[t]
     int pick = -1;
     if (!p.stacked && k > n) {
         pick = l < n ? l : -1;
@@ -473,8 +619,6 @@ __device__ __forceinline__ bool attack_one(const Params& p, Rng& rng, Lane& L, i
         pick = l < k ? perm : -1;
         nlist = k;
     }
-    // translate ranks to lanes
-    list = -1;
     for (int t = 0; t < nlist; t++) {
         const int pr = rl(pick, t);
         const int lane_t = first_lane(__ballot(rank == pr));
@@ -484,20 +628,25 @@ __device__ __forceinline__ bool attack_one(const Params& p, Rng& rng, Lane& L, i
     const double strength = rld(L.strength, a);
     for (int t = 0; t < nlist; t++) {
         const int b = rl(list, t);
-        if (l == b && L.active) {
+        if (!rlb(L.active, b)) continue;                    // already dead: skipped
+        if (l == b) {
             double h = L.health - strength;
             if (0.0 > h) h = 0.0;
             if (1.0 < h) h = 1.0;
             L.health = h;
             L.active = h > 0.0;
-            if (!L.active) L.in_grid = false;               // grid.remove
+        }
+        if (!rlb(L.active, b)) {                            // grid.remove
+            const int br = rl(L.r, b), bc = rl(L.c, b);
+            if (l == b) L.in_grid = false;
+            table_remove(p, sm, L, b, br, bc);
         }
     }
     return true;
 }
 
-// MoveActor.process_action
-__device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr, int mc, uint32_t& ctr)
+// MoveActor.process_action, serial form (Grid.query as a ballot)
+__device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr, int mc, uint32_t newseq)
 {
     const int l = lane_id();
     const uint32_t akind = rl(L.kind, a);
@@ -509,8 +658,7 @@ __device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr
     const uint32_t aov = rl(L.ov, a);
     const bool blocks = l < p.A && L.in_grid && L.r == nr && L.c == nc && !((aov >> L.enc) & 1u);
     if (__ballot(blocks)) return false;                     // Grid.query
-    if (l == a) { L.r = nr; L.c = nc; L.seq = ctr; }        // remove + place (appended)
-    ctr++;
+    if (l == a) { L.r = nr; L.c = nc; L.seq = newseq; }     // remove + place (appended)
     return true;
 }
 
@@ -521,159 +669,30 @@ __device__ __forceinline__ void renorm_seq(const Params& p, Lane& L, uint32_t& c
     uint32_t rank = 0;
     for (int i = 0; i < p.A; i++) {
         uint32_t si = rl(L.seq, i);
-        bool gi = __builtin_amdgcn_readlane((int)L.in_grid, i);
+        bool gi = rlb(L.in_grid, i);
         if (gi && si < L.seq) rank++;
     }
     if (l < p.A && L.in_grid) L.seq = rank;
-    ctr = (uint32_t)__popcll(__ballot(l < p.A && L.in_grid));
+    ctr = (uint32_t)p.A;
 }
 
-// ------------------------------------------------------------ kernels
-template <int S>
-__global__ __launch_bounds__(WAVE) void step_kernel(Params p)
+// ------------------------------------------------------------ reset
+// AllStepManager.reset (all_step_manager.py:37-49) -> SmartGWS.reset ->
+// PositionState.reset (state.py:88-166) / HealthState.reset (:629-641) in the
+// pinned order.  Returns false on the reference's placement exceptions.
+__device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr, uint32_t& err)
 {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int e = blockIdx.x;
-    if (e >= p.E) return;
-    constexpr int SS = S * S;
-    const int l = lane_id();
-    const int A = p.A;
-    const bool valid = l < A;
-    Smem sm = carve(smem_raw, p.H * p.W, A, SS);
-    Lane L;
-    load_lane(p, e, L, valid);
-    Rng rng;
-    load_rng(p, e, sm, rng);
-    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
-    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
-
-    // actions (lane = agent); attack == -1 marks "not in action_dict"
-    int mr = 0, mc = 0, ak = -1;
-    if (valid) {
-        const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
-        mr = ap[0]; mc = ap[1]; ak = ap[2];
-    }
-    const bool acting = valid && L.live && ak >= 0;
-    const uint64_t act_mask = __ballot(acting);
-
-    if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
-        // attack pass (team_battle_example.py:35-47)
-        // the active check is re-evaluated per attacker: earlier attacks can kill
-        for (uint64_t it = act_mask; it; it &= it - 1) {
-            const int a = first_lane(it);
-            if (!rl((int)L.active, a)) continue;
-            int nlist, list;
-            const bool status = attack_one(p, rng, L, a, rl(ak, a), nlist, list);
-            if (status) {
-                if (nlist == 0) { if (l == a) L.reward -= 0.1; }
-                else {
-                    for (int t = 0; t < nlist; t++) {
-                        const int b = rl(list, t);
-                        const bool dead = !rl((int)L.active, b);
-                        if (dead) {
-                            if (l == b) L.reward -= 1.0;
-                            if (l == a) L.reward += 1.0;
-                        }
-                    }
-                }
-            }
-        }
-        // move pass (:50-55)
-        for (uint64_t it = act_mask; it; it &= it - 1) {
-            const int a = first_lane(it);
-            if (!rl((int)L.active, a)) continue;
-            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr);
-            if (!ok && l == a) L.reward -= 0.1;
-        }
-        // entropy (:58-59)
-        if (acting) L.reward -= 0.01;
-    } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        const int n = p.nav, t = p.target;
-        if ((act_mask >> n) & 1) {
-            const bool ok = move_one(p, L, n, rl(mr, n), rl(mc, n), ctr);
-            if (!ok && l == n) L.reward -= 0.1;
-            const bool at = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
-            if (at && l == n) L.reward += 1.0;
-            if (l == n) L.reward -= 0.01;
-        }
-    }
-
-    // observations of the live agents (all_step_manager.py:68-71)
-    build_cells(p, sm, L);
-    observe_all<S>(p, e, sm, rng, L);
-
-    // rewards, dones (:72-79, smart.py:101-111)
-    bool dn;
-    if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        const int n = p.nav, t = p.target;
-        dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
-    } else {
-        dn = !L.active;
-    }
-    if (valid) {
-        size_t k = (size_t)e * A + l;
-        p.reward[k] = L.live ? L.reward : 0.0;
-        p.done[k] = L.live ? (uint8_t)dn : (uint8_t)1;
-    }
-    const bool live_after = valid && L.live && !dn;
-    // get_all_done (done.py:49-56,147-153) or maze target reached
-    bool all;
-    if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        all = dn;
-    } else {
-        all = true;
-        if (p.done_kind & GW_DONE_ACTIVE) all = all && (__ballot(valid && L.active) == 0);
-        if (p.done_kind & GW_DONE_ONE_TEAM) {
-            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u);
-            all = all && (__popc(bits) <= 1);
-        }
-    }
-    const bool any_left = __ballot(live_after) != 0;
-    L.live = live_after;
-    if (l == 0) {
-        p.all_done[e] = (uint8_t)(all || !any_left);
-        p.steps[e] += 1;
-        if (p.acting) p.acting[e] += (uint64_t)__popcll(act_mask);
-    }
-    store_lane(p, e, L, valid);
-    store_rng(p, e, sm, rng, ctr);
-}
-
-template <int S>
-__global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int e = blockIdx.x;
-    if (e >= p.E) return;
-    // reset everything when no selector is given; otherwise the union of the
-    // explicit mask, the previous step's __all__ and the horizon
-    bool go;
-    if (p.mask == nullptr && p.prev_all_done == nullptr && p.horizon <= 0) go = true;
-    else go = (p.mask && p.mask[e]) || (p.prev_all_done && p.prev_all_done[e]) ||
-              (p.horizon > 0 && p.steps[e] >= p.horizon);
-    if (!go) return;
-
-    constexpr int SS = S * S;
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
     const int HW = p.H * p.W;
-    Smem sm = carve(smem_raw, HW, A, SS);
-    Lane L;
-    load_lane(p, e, L, valid);
-    Rng rng;
-    load_rng(p, e, sm, rng);
-    uint32_t ctr = 0;
-    uint32_t err = 0;
-
-    // AllStepManager.reset: done_agents = non-Agent entities
     L.live = valid && (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
     L.in_grid = false;
     L.reward = 0.0;
+    ctr = 0;
     const bool has_health = __ballot(valid && (L.kind & GW_K_HEALTH)) != 0;
 
     auto health_reset = [&]() {
-        // state.py:629-641, agent order, one uniform() per random health
         for (int a = 0; a < A; a++) {
             const uint32_t k = rl(L.kind, a);
             if (!(k & GW_K_HEALTH)) continue;
@@ -686,8 +705,8 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
     };
 
     auto position_reset = [&]() -> bool {
-        // state.py:88-166 — availability lists are bitmaps (the reference's
-        // lists stay in ascending cell order under list.remove)
+        // availability lists -> bitmaps (the lists stay in ascending cell
+        // order under list.remove); lane w holds word w of each bitmap
         const int nwords = (HW + 63) / 64;
         for (int enc = 1; enc <= p.max_enc; enc++) {
             uint64_t w = 0;
@@ -708,19 +727,15 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
                 if (has_ip) { r = ir; c = ic; }
                 else {
                     const uint64_t w = (l < nwords) ? sm.avail[aenc * 64 + l] : 0ull;
-                    const uint32_t pc = (l < nwords) ? (uint32_t)__popcll(w) : 0u;
+                    const uint32_t pc = (uint32_t)__popcll(w);
                     const uint32_t incl = wave_incl_scan(pc);
                     const uint32_t total = rl(incl, WAVE - 1);
                     if (total == 0) { err |= GW_ERR_NO_CELL; return false; }
                     const uint32_t idx = rng.interval(total - 1);
                     const uint32_t excl = incl - pc;
-                    const bool mine = l < nwords && excl <= idx && idx < incl;
+                    const bool mine = pc != 0 && excl <= idx && idx < incl;
                     int cell = 0;
-                    if (mine) {
-                        uint64_t ww = w;
-                        for (uint32_t t = excl; t < idx; t++) ww &= ww - 1;
-                        cell = l * 64 + (int)__builtin_ctzll(ww);
-                    }
+                    if (mine) cell = l * 64 + select_bit(w, idx - excl);
                     cell = rl(cell, first_lane(__ballot(mine)));
                     r = cell / p.W; c = cell % p.W;
                 }
@@ -751,20 +766,229 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
         if (has_health) health_reset();
         ok = position_reset();
     }
-    // agents without HealthAgent keep active = True
-    if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;
+    if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
+    return ok;
+}
 
+template <int S>
+__device__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr)
+{
+    constexpr int SS = S * S;
+    uint32_t err = 0;
+    const bool ok = do_reset(p, sm, rng, L, ctr, err);
     if (ok) {
-        build_cells(p, sm, L);
+        build_tables(p, sm, L);
         observe_all<S>(p, e, sm, rng, L);
     } else {
-        int32_t* out = p.obs + (size_t)e * A * SS;
-        for (int i = l; i < A * SS; i += WAVE) out[i] = -2;
+        int32_t* out = p.obs + (size_t)e * p.A * SS;
+        for (int i = lane_id(); i < p.A * SS; i += WAVE) out[i] = -2;
     }
-    if (l == 0) {
+    if (lane_id() == 0) {
         p.steps[e] = 0;
         if (p.err) p.err[e] |= err;
     }
+}
+
+// ------------------------------------------------------------ kernels
+template <int S>
+__global__ __launch_bounds__(WAVE) void step_kernel(Params p)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int e = blockIdx.x;
+    if (e >= p.E) return;
+    const int l = lane_id();
+    const int A = p.A;
+    const bool valid = l < A;
+    STAMP(0);
+    Smem sm = carve(smem_raw, p);
+    Lane L;
+    load_lane(p, e, L, valid);
+    Rng rng;
+    load_rng(p, e, sm, rng);
+    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
+    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
+
+    // actions (lane = agent); attack == -1 marks "not in action_dict"
+    int mr = 0, mc = 0, ak = -1;
+    if (valid) {
+        const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
+        mr = ap[0]; mc = ap[1]; ak = ap[2];
+    }
+    const bool acting = valid && L.live && ak >= 0;
+    const uint64_t act_mask = __ballot(acting);
+    build_tables(p, sm, L);
+    STAMP(1);
+
+    if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
+        // ---- attack pass (team_battle_example.py:35-47)
+        const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
+        const bool maybe = att && L.active && attack_precheck(p, sm, L);
+        const uint64_t maybe_mask = __ballot(maybe);
+        for (uint64_t it = __ballot(att); it; it &= it - 1) {
+            const int a = first_lane(it);
+            if (!rlb(L.active, a)) continue;                // killed earlier this pass
+            if (!((maybe_mask >> a) & 1)) {                  // no possible target: (True, [])
+                if (l == a) L.reward -= 0.1;
+                continue;
+            }
+            int nlist, list;
+            attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+            if (nlist == 0) { if (l == a) L.reward -= 0.1; }
+            else {
+                for (int t = 0; t < nlist; t++) {
+                    const int b = rl(list, t);
+                    if (!rlb(L.active, b)) {
+                        if (l == b) L.reward -= 1.0;
+                        if (l == a) L.reward += 1.0;
+                    }
+                }
+            }
+        }
+        STAMP(2);
+        // ---- move pass (:50-55)
+        const bool mover = acting && L.active;
+        const bool can_move = mover && (L.kind & GW_K_MOVING);
+        const int nr = L.r + mr, nc = L.c + mc;
+        const bool inb = 0 <= nr && nr < p.H && 0 <= nc && nc < p.W;
+        const bool stay = nr == L.r && nc == L.c;
+        const bool real = can_move && inb && !stay;
+        // isolation: no other mover targets my source or target, none leaves my target
+        const int HW = p.H * p.W;
+        const int nw = (HW + 3) / 4;
+        for (int i = l; i < nw; i += WAVE) { sm.tcnt[i] = 0u; sm.scnt[i] = 0u; }
+        wave_sync();
+        const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
+        if (real) {
+            atomicAdd(&sm.tcnt[tgt >> 2], 1u << (8 * (tgt & 3)));
+            atomicAdd(&sm.scnt[src >> 2], 1u << (8 * (src & 3)));
+        }
+        wave_sync();
+        bool iso = false, iso_ok = false;
+        if (real && cnt_get(sm.tcnt, tgt) == 1 && cnt_get(sm.scnt, tgt) == 0 &&
+            cnt_get(sm.tcnt, src) == 0) {
+            const uint32_t b = sm.tbl[tbl_idx(p, nr, nc)];
+            if (b != CELL_CROWD) { iso = true; iso_ok = (b == 0) || ((L.ov >> b) & 1u); }
+        }
+        const int pr = L.r, pc = L.c;
+        bool moved = false;
+        if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)l; moved = true; }
+        bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
+        for (uint64_t it = __ballot(real && !iso); it; it &= it - 1) {
+            const int a = first_lane(it);
+            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+            if (l == a) { fail = !ok; moved = ok; }
+        }
+        if (fail) L.reward -= 0.1;
+        ctr += (uint32_t)WAVE;
+        // ---- entropy (:58-59)
+        if (acting) L.reward -= 0.01;
+        // cell table after the moves
+        wave_sync();
+        if (moved) {
+            const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
+            atomicSub(&sm.cnt[oc >> 2], 1u << (8 * (oc & 3)));
+            atomicAdd(&sm.cnt[ncl >> 2], 1u << (8 * (ncl & 3)));
+            sm.tbl[tbl_idx(p, pr, pc)] = 0;
+        }
+        wave_sync();
+        if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
+        wave_sync();
+    } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        const int n = p.nav, t = p.target;
+        if ((act_mask >> n) & 1) {
+            const int pr = rl(L.r, n), pc = rl(L.c, n);
+            const bool ok = move_one(p, L, n, rl(mr, n), rl(mc, n), ctr + (uint32_t)n);
+            if (!ok && l == n) L.reward -= 0.1;
+            const bool at = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+            if (at && l == n) L.reward += 1.0;
+            if (l == n) L.reward -= 0.01;
+            ctr += (uint32_t)WAVE;
+            const int qr = rl(L.r, n), qc = rl(L.c, n);
+            if (ok && (qr != pr || qc != pc)) {
+                table_remove(p, sm, L, n, pr, pc);
+                const int ncl = qr * p.W + qc;
+                if (l == n) atomicAdd(&sm.cnt[ncl >> 2], 1u << (8 * (ncl & 3)));
+                wave_sync();
+                if (L.in_grid && L.r == qr && L.c == qc)
+                    sm.tbl[tbl_idx(p, qr, qc)] = cell_byte(cnt_get(sm.cnt, ncl), L.enc);
+                wave_sync();
+            }
+        }
+    }
+    STAMP(3);
+
+    // ---- observations of the live agents (all_step_manager.py:68-71)
+    STAMP(4);
+    observe_all<S>(p, e, sm, rng, L);
+    STAMP(5);
+
+    // ---- rewards, dones (:72-79, smart.py:101-111)
+    bool dn;
+    if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        const int n = p.nav, t = p.target;
+        dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+    } else {
+        dn = !L.active;
+    }
+    if (valid) {
+        size_t k = (size_t)e * A + l;
+        p.reward[k] = L.live ? L.reward : 0.0;
+        p.done[k] = L.live ? (uint8_t)dn : (uint8_t)1;
+    }
+    const bool live_after = valid && L.live && !dn;
+    // get_all_done (done.py:49-56,147-153) or maze target reached
+    bool all;
+    if (p.sim_kind == GW_SIM_MAZE_NAV) {
+        all = dn;
+    } else {
+        all = true;
+        if (p.done_kind & GW_DONE_ACTIVE) all = all && (__ballot(valid && L.active) == 0);
+        if (p.done_kind & GW_DONE_ONE_TEAM) {
+            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u);
+            all = all && (__popc(bits) <= 1);
+        }
+    }
+    const bool any_left = __ballot(live_after) != 0;
+    L.live = live_after;
+    const bool all_done = all || !any_left;
+    const int32_t steps = p.steps[e] + 1;
+    if (l == 0) {
+        p.all_done[e] = (uint8_t)all_done;
+        p.steps[e] = steps;
+        if (p.acting) p.acting[e] += (uint64_t)__popcll(act_mask);
+    }
+    // ---- fused auto-reset: the next episode's first observation replaces obs
+    if (p.autoreset && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
+        wave_sync();
+        reset_env<S>(p, e, sm, rng, L, ctr);
+    }
+    store_lane(p, e, L, valid);
+    store_rng(p, e, sm, rng, ctr);
+    STAMP(6);
+}
+
+template <int S>
+__global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int e = blockIdx.x;
+    if (e >= p.E) return;
+    // reset everything when no selector is given; otherwise the union of the
+    // explicit mask, the previous step's __all__ and the horizon
+    bool go;
+    if (p.mask == nullptr && p.prev_all_done == nullptr && p.horizon <= 0) go = true;
+    else go = (p.mask && p.mask[e]) || (p.prev_all_done && p.prev_all_done[e]) ||
+              (p.horizon > 0 && p.steps[e] >= p.horizon);
+    if (!go) return;
+    const int l = lane_id();
+    const bool valid = l < p.A;
+    Smem sm = carve(smem_raw, p);
+    Lane L;
+    load_lane(p, e, L, valid);
+    Rng rng;
+    load_rng(p, e, sm, rng);
+    uint32_t ctr = 0;
+    reset_env<S>(p, e, sm, rng, L, ctr);
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
 }
@@ -978,9 +1202,20 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
     for (int i = 0; i <= GW_MAX_ENC; i++) { p.overlap[i] = cfg->overlap[i]; p.amap[i] = cfg->attack_mapping[i]; }
+    // padded cell table: border = max(view range, attack ranges); rows are
+    // read as dwords, so the pitch is a multiple of 4 with slack for the
+    // over-read, plus one slack row at the end
+    int pad = cfg->obs_range;
+    for (int a = 0; a < A; a++)
+        if ((cfg->agents[a].kind & GW_K_ATTACKING) && cfg->agents[a].attack_range > pad)
+            pad = cfg->agents[a].attack_range;
+    p.pad = pad;
+    p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 6) / 4);
+    p.tbl_rows = cfg->rows + 2 * pad + 1;
     const int SS = g->S * g->S;
-    g->smem_step = smem_bytes(HW, A, SS, max_enc, false);
-    g->smem_reset = smem_bytes(HW, A, SS, max_enc, true);
+    g->smem_step = smem_bytes(HW, A, SS, max_enc, p.tbl_rows * p.pitch);
+    g->smem_reset = g->smem_step;
+    if (g->smem_step > 160 * 1024) { set_err("LDS need %zu B > 160 KiB", g->smem_step); return GW_E_UNSUPPORTED; }
     HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
     *out = g;
     return GW_OK;
@@ -1025,6 +1260,22 @@ gw_status gw_step(gw_handle g, const int32_t* actions, int32_t* obs, double* rew
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.acting = acting;
+    p.autoreset = 0;
+    HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_step_autoreset(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
+                            uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
+                            uint32_t* err_flags, void* stream)
+{
+    if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.acting = acting;
+    p.autoreset = 1;
+    p.horizon = horizon;
+    p.err = err_flags;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
     return GW_OK;
 }
@@ -1056,6 +1307,14 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     if (seq) HIPCHK(hipMemcpyAsync(g->base.seq, seq, EA * 4, hipMemcpyDeviceToDevice, st));
     if (mt) HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
     if (steps) HIPCHK(hipMemcpyAsync(g->base.steps, steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
+// diagnostic hook (not in the public header): stamps buffer for -DGW_STAMPS builds
+gw_status gw_debug_set_stamps(gw_handle g, uint64_t* stamps)
+{
+    if (!g) return GW_E_INVALID;
+    g->base.stamps = stamps;
     return GW_OK;
 }
 

@@ -91,6 +91,19 @@ class GridWorldEngine:
                                          _stream()), 'gw_step')
         return self.obs, self.reward, self.done, self.all_done
 
+    def step_autoreset(self, actions=None, horizon=0):
+        """step() + in-launch reset of the envs whose '__all__' is set or that
+        reached `horizon`: their obs is the next episode's first observation,
+        reward/done/all_done the terminal step's."""
+        a = self.actions if actions is None else actions
+        assert a.dtype == torch.int32 and a.is_contiguous() and a.shape == self.actions.shape
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_step_autoreset(
+                self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                _ptr(self.all_done), _ptr(self.acting), int(horizon), _ptr(self.err), _stream()),
+                'gw_step_autoreset')
+        return self.obs, self.reward, self.done, self.all_done
+
     def random_actions(self, key, step, env_offset=0, out=None):
         """Synthetic random policy (Philox, keyed by key / global env / step / agent)."""
         out = self.actions if out is None else out

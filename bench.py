@@ -4,8 +4,8 @@ Workload (BASELINE.json configs[2], the metric's config): TeamBattle 32x32,
 64 BattleAgents in 2 teams, 4096 envs per GPU (weak scaling: N GPUs run
 N x 4096 envs, sharded by global env id, no data-path collective), horizon
 200 with on-device auto-reset.  One timed "step" = random-policy actions
-(Philox kernel) + the fused AllStepManager.step kernel + the masked
-auto-reset kernel, for every env.
+(Philox kernel) + the fused AllStepManager.step kernel with in-launch
+auto-reset of finished episodes, for every env.
 
 Metric: agent-steps/s = sum over env-steps of the acting (not-done) agents,
 the reference's len(action_dict), over all ranks / the max
@@ -122,10 +122,9 @@ def main():
         eng.random_actions(key, t, env_offset=first)
         if ev is not None:
             ev[0].record()
-        eng.step()
+        eng.step_autoreset(horizon=args.horizon)
         if ev is not None:
             ev[1].record()
-        eng.reset(all_done=eng.all_done, horizon=args.horizon)
 
     for t in range(args.warmup):
         one_step(t)

@@ -154,6 +154,15 @@ gw_status gw_reset(gw_handle h, const uint8_t* mask, const uint8_t* all_done,
 gw_status gw_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
                   uint8_t* done, uint8_t* all_done, uint64_t* acting, void* stream);
 
+/* gw_step followed, in the same launch, by AllStepManager.reset of every env
+   whose '__all__' is set or that reached `horizon` steps (horizon > 0).  For
+   those envs obs holds the first observation of the next episode, while
+   reward / done / all_done are the terminal step's (RLlib VectorEnv
+   auto-reset convention).  err_flags: device uint32[E] or NULL.            */
+gw_status gw_step_autoreset(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
+                            uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
+                            uint32_t* err_flags, void* stream);
+
 /* Snapshot / restore of the engine state (device buffers, caller-owned).
      pos     int32[E][A][2]   (row, col)
      health  double[E][A]

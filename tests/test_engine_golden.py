@@ -42,3 +42,26 @@ class EngineRunner:
 def test_engine_matches_reference(name):
     g = load_golden(name)
     replay(EngineRunner(g), g)
+
+
+@pytest.mark.parametrize('name', GOLDEN_CASES)
+def test_engine_autoreset_matches_reference(name):
+    """gw_step_autoreset: terminal reward/done/__all__, and for reset envs the
+    next episode's first observation, against the same fixtures."""
+    import torch
+    g = load_golden(name)
+    run = EngineRunner(g)
+    eng = run.eng
+    obs0 = run.reset(None)
+    assert (obs0 == g['obs0']).all()
+    c = g['case']
+    for t in range(g['actions'].shape[0]):
+        a = torch.as_tensor(g['actions'][t].astype(np.int32), device=eng.device).contiguous()
+        obs, rew, done, ad = eng.step_autoreset(a, horizon=c['horizon'])
+        obs, rew, done, ad = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), ad.cpu().numpy()
+        m = g['reset_mask'][t].astype(bool)
+        want = np.where(m[:, None, None, None], g['reset_obs'][t], g['obs'][t])
+        assert (obs == want).all(), f"step {t}: obs"
+        assert (rew.view(np.uint64) == g['reward'][t].view(np.uint64)).all(), f"step {t}: reward"
+        assert (done == g['done'][t]).all() and (ad == g['all_done'][t]).all(), f"step {t}: done"
+    assert not eng.err.any().item()

@@ -1,0 +1,63 @@
+"""Diagnostic: per-phase cycle shares of step_kernel from s_memtime stamps.
+
+Builds/loads libgw_engine_stamps.so (-DGW_STAMPS), runs the bench workload
+and prints the median cycles between consecutive stamps over envs & steps.
+Read the SHARES, not the absolute time (stamps serialise the schedule).
+usage (GPU): GW_ENGINE_STAMPS=1 python tools/stamps.py
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ['GW_ENGINE_STAMPS'] = '1'
+
+from abmarl_amd import _native  # noqa: E402
+_native.build(stamps=True)
+from abmarl_amd.engine import GridWorldEngine, env_seeds  # noqa: E402
+import bench  # noqa: E402
+
+NAMES = {0: 'start', 1: 'load', 2: 'attack', 3: 'move', 4: 'cells', 8: 'obs-par', 9: 'obs-ev',
+         5: 'obs-store', 6: 'dones+store'}
+
+
+def main():
+    cc = bench.team_battle_sim().compiled()
+    E = int(os.environ.get('ENVS', '4096'))
+    eng = GridWorldEngine(cc, E, seeds=env_seeds(E))
+    L = eng.L
+    L.gw_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    st = torch.zeros((E, 16), dtype=torch.int64, device=eng.device)
+    L.gw_debug_set_stamps(eng.h, C.c_void_p(st.data_ptr()))
+    eng.reset()
+    order = [0, 1, 2, 3, 4, 8, 9, 5, 6]
+    deltas = []
+    ends = []
+    for t in range(200):
+        eng.random_actions(7, t)
+        st.zero_()
+        eng.step()
+        torch.cuda.synchronize()
+        s = st.cpu().numpy()
+        if t >= 20:
+            d = np.stack([s[:, order[i + 1]] - s[:, order[i]] for i in range(len(order) - 1)], 1)
+            deltas.append(d)
+            ends.append(s[:, 6] - s[:, 0].min())
+        eng.reset(all_done=eng.all_done, horizon=200)
+    d = np.concatenate(deltas)
+    tot = d.sum(1)
+    print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
+          f"{np.percentile(tot, 90):.0f} max {tot.max()}")
+    for i in range(len(order) - 1):
+        print(f"  {NAMES[order[i]]:>8s} -> {NAMES[order[i+1]]:<12s} median {np.median(d[:, i]):8.0f}"
+              f"  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum() * 100:5.1f}%")
+    e = np.concatenate(ends)
+    print(f"env end time since first start: median {np.median(e):.0f} max {e.max()}")
+
+
+if __name__ == '__main__':
+    main()
