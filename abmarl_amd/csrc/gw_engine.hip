@@ -442,7 +442,7 @@ __device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const La
 {
     constexpr int SS = S * S;
     constexpr int R = S / 2;
-    constexpr int ND = (S + 3 + 3) / 4;       // dwords covering S bytes at any alignment
+    constexpr int ND = (S + 3) / 4 + 1;       // dwords covering S bytes at any alignment
     const int l = lane_id();
     const int A = p.A;
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
@@ -1210,7 +1210,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         if ((cfg->agents[a].kind & GW_K_ATTACKING) && cfg->agents[a].attack_range > pad)
             pad = cfg->agents[a].attack_range;
     p.pad = pad;
-    p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 6) / 4);
+    p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 3) / 4 + 1);
     p.tbl_rows = cfg->rows + 2 * pad + 1;
     const int SS = g->S * g->S;
     g->smem_step = smem_bytes(HW, A, SS, max_enc, p.tbl_rows * p.pitch);
