@@ -40,6 +40,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include "../../include/gw_engine.h"
 
@@ -78,6 +79,7 @@ struct Params {
     int32_t observe_self, stacked, no_overlap_at_reset, state_order;
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
+    const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
 };
@@ -394,21 +396,9 @@ __device__ void build_tables(const Params& p, Smem& sm, const Lane& L)
     const int l = lane_id();
     const int HW = p.H * p.W;
     const int nw = (HW + 3) / 4;
-    // border = 0xFF, interior = 0 (pitch is a multiple of 4: a dword never spans rows)
-    const int tdw = p.tbl_rows * p.pitch / 4;
-    uint32_t* t32 = (uint32_t*)sm.tbl;
-    for (int i = l; i < tdw; i += WAVE) {
-        const int row = (i * 4) / p.pitch - p.pad;
-        const int col0 = (i * 4) % p.pitch - p.pad;
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int col = col0 + b;
-            const bool off = row < 0 || row >= p.H || col < 0 || col >= p.W;
-            w |= (off ? CELL_OFF : 0u) << (8 * b);
-        }
-        t32[i] = w;
-    }
+    // border = 0xFF, interior = 0: copy of the per-config template (L2-resident)
+    const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
+    for (int i = l; i < t16; i += WAVE) ((uint4*)sm.tbl)[i] = p.tbl_tmpl[i];
     for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
     wave_sync();
     int cell = L.r * p.W + L.c;
@@ -693,6 +683,38 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
     const bool has_health = __ballot(valid && (L.kind & GW_K_HEALTH)) != 0;
 
     auto health_reset = [&]() {
+        // one uniform() per HealthAgent without initial_health, in agent order:
+        // consecutive word pairs of the stream, drawn lane-parallel when no
+        // twist falls inside the batch
+        const bool hl = valid && (L.kind & GW_K_HEALTH);
+        const bool randh = hl && !(L.init_health >= 0.0);
+        const uint64_t rm = __ballot(randh);
+        const int nrand = __popcll(rm);
+        if (rng.pos + 2 * nrand <= GW_MT_N) {
+            if (hl) {
+                double h = L.init_health;
+                if (randh) {
+                    const int k = __popcll(rm & ((1ull << l) - 1));
+                    uint32_t w[2];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        uint32_t y = rng.key[rng.pos + 2 * k + q];
+                        y ^= (y >> 11);
+                        y ^= (y << 7) & 0x9d2c5680u;
+                        y ^= (y << 15) & 0xefc60000u;
+                        y ^= (y >> 18);
+                        w[q] = y;
+                    }
+                    h = ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6)) / 9007199254740992.0;
+                }
+                if (0.0 > h) h = 0.0;
+                if (1.0 < h) h = 1.0;
+                L.health = h;
+                L.active = h > 0.0;
+            }
+            rng.pos += 2 * nrand;
+            return;
+        }
         for (int a = 0; a < A; a++) {
             const uint32_t k = rl(L.kind, a);
             if (!(k & GW_K_HEALTH)) continue;
@@ -702,6 +724,79 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
             if (1.0 < h) h = 1.0;
             if (l == a) { L.health = h; L.active = h > 0.0; }
         }
+    };
+
+    // PositionState with <= 4 encodings: the availability bitmaps live in
+    // registers (lane w holds word w), with each lane's inclusive prefix
+    // popcount and the per-encoding totals maintained incrementally, so a
+    // placement is one draw, one ballot and a handful of lane-local updates.
+    constexpr int ME = 4;
+    auto position_reset_regs = [&]() -> bool {
+        const int nwords = (HW + 63) / 64;
+        uint64_t av[ME + 1];
+        uint32_t pcnt[ME + 1], incl[ME + 1], total[ME + 1];
+        uint64_t full = 0;
+        if (l < nwords) {
+            const int rem = HW - l * 64;
+            full = rem >= 64 ? ~0ull : ((1ull << rem) - 1);
+        }
+        const uint32_t fpc = (uint32_t)__popcll(full);
+        const uint32_t fincl = wave_incl_scan(fpc);
+#pragma unroll
+        for (int f = 0; f <= ME; f++) {
+            av[f] = (f >= 1 && f <= p.max_enc) ? full : 0ull;
+            pcnt[f] = (f >= 1 && f <= p.max_enc) ? fpc : 0u;
+            incl[f] = (f >= 1 && f <= p.max_enc) ? fincl : 0u;
+            total[f] = (f >= 1 && f <= p.max_enc) ? (uint32_t)HW : 0u;
+        }
+        for (int pass = 0; pass < 2; pass++) {
+            for (int a = 0; a < A; a++) {
+                const int ir = rl(L.init_r, a), ic = rl(L.init_c, a);
+                const bool has_ip = ir >= 0;
+                if ((pass == 0) != has_ip) continue;
+                const int aenc = rl(L.enc, a);
+                const uint32_t aov = rl(L.ov, a);
+                int cell;
+                if (has_ip) {
+                    cell = ir * p.W + ic;
+                    // Grid.place -> query (grid.py:81-129); asserted by the reference
+                    const bool blocks = valid && L.in_grid && L.r == ir && L.c == ic &&
+                                        !((aov >> L.enc) & 1u);
+                    if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
+                } else {
+                    uint64_t w = 0; uint32_t pc = 0, inc = 0, tot = 0;
+#pragma unroll
+                    for (int f = 1; f <= ME; f++)
+                        if (aenc == f) { w = av[f]; pc = pcnt[f]; inc = incl[f]; tot = total[f]; }
+                    if (tot == 0) { err |= GW_ERR_NO_CELL; return false; }
+                    const uint32_t idx = rng.interval(tot - 1);   // np.random.choice(list, 1)
+                    const uint32_t excl = inc - pc;
+                    const bool mine = pc != 0 && excl <= idx && idx < inc;
+                    int c0 = 0;
+                    if (mine) c0 = l * 64 + select_bit(w, idx - excl);
+                    cell = rl(c0, first_lane(__ballot(mine)));
+                    // cells from the availability list always pass Grid.query
+                }
+                const int r = cell / p.W, c = cell % p.W;
+                if (l == a) { L.r = r; L.c = c; L.in_grid = true; L.seq = ctr; }
+                ctr++;
+                // _update_available_positions (state.py:126-141)
+                const int wl = cell >> 6;
+                const uint64_t bit = 1ull << (cell & 63);
+#pragma unroll
+                for (int f = 1; f <= ME; f++) {
+                    if (f > p.max_enc) continue;
+                    if (!(p.no_overlap_at_reset || !((aov >> f) & 1u))) continue;
+                    const bool was = l == wl && (av[f] & bit) != 0;
+                    if (__ballot(was)) {                         // cell still listed
+                        if (l == wl) { av[f] &= ~bit; pcnt[f] -= 1; }
+                        if (l >= wl) incl[f] -= 1;
+                        total[f] -= 1;
+                    }
+                }
+            }
+        }
+        return true;
     };
 
     auto position_reset = [&]() -> bool {
@@ -758,13 +853,16 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
         return true;
     };
 
+    auto place = [&]() -> bool {
+        return p.max_enc <= ME ? position_reset_regs() : position_reset();
+    };
     bool ok;
     if (p.state_order == GW_ORDER_POSITION_HEALTH) {
-        ok = position_reset();
+        ok = place();
         if (ok && has_health) health_reset();
     } else {
         if (has_health) health_reset();
-        ok = position_reset();
+        ok = place();
     }
     if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
     return ok;
@@ -776,6 +874,7 @@ __device__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, u
     constexpr int SS = S * S;
     uint32_t err = 0;
     const bool ok = do_reset(p, sm, rng, L, ctr, err);
+    STAMP(13);
     if (ok) {
         build_tables(p, sm, L);
         observe_all<S>(p, e, sm, rng, L);
@@ -816,6 +915,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     }
     const bool acting = valid && L.live && ak >= 0;
     const uint64_t act_mask = __ballot(acting);
+    STAMP(10);
     build_tables(p, sm, L);
     STAMP(1);
 
@@ -960,7 +1060,9 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     // ---- fused auto-reset: the next episode's first observation replaces obs
     if (p.autoreset && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
         wave_sync();
+        STAMP(12);
         reset_env<S>(p, e, sm, rng, L, ctr);
+        STAMP(14);
     }
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
@@ -1047,6 +1149,7 @@ struct gw_engine {
     int E, A, H, W, S, max_enc;
     Params base;
     DevAgent* d_spec;
+    uint4* d_tmpl;
     size_t smem_step, smem_reset;
 };
 
@@ -1212,6 +1315,18 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.pad = pad;
     p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 3) / 4 + 1);
     p.tbl_rows = cfg->rows + 2 * pad + 1;
+    {
+        const size_t tb = align16((size_t)p.tbl_rows * p.pitch);
+        uint8_t* ht = (uint8_t*)malloc(tb);
+        for (size_t i = 0; i < tb; i++) {
+            const int row = (int)(i / p.pitch) - pad, col = (int)(i % p.pitch) - pad;
+            ht[i] = (row < 0 || row >= cfg->rows || col < 0 || col >= cfg->cols) ? CELL_OFF : 0;
+        }
+        HIPCHK(hipMalloc(&g->d_tmpl, tb));
+        HIPCHK(hipMemcpy(g->d_tmpl, ht, tb, hipMemcpyHostToDevice));
+        free(ht);
+        p.tbl_tmpl = g->d_tmpl;
+    }
     const int SS = g->S * g->S;
     g->smem_step = smem_bytes(HW, A, SS, max_enc, p.tbl_rows * p.pitch);
     g->smem_reset = g->smem_step;
@@ -1226,7 +1341,7 @@ gw_status gw_destroy(gw_handle g)
     if (!g) return GW_E_INVALID;
     (void)hipFree(g->base.pos); (void)hipFree(g->base.health); (void)hipFree(g->base.flags);
     (void)hipFree(g->base.seq); (void)hipFree(g->base.mt); (void)hipFree(g->base.steps);
-    (void)hipFree(g->d_spec);
+    (void)hipFree(g->d_spec); (void)hipFree(g->d_tmpl);
     delete g;
     return GW_OK;
 }

@@ -21,7 +21,7 @@ _native.build(stamps=True)
 from abmarl_amd.engine import GridWorldEngine, env_seeds  # noqa: E402
 import bench  # noqa: E402
 
-NAMES = {0: 'start', 1: 'load', 2: 'attack', 3: 'move', 4: 'cells', 8: 'obs-par', 9: 'obs-ev',
+NAMES = {0: 'start', 1: 'tables', 10: 'load', 2: 'attack', 3: 'move', 4: 'cells', 8: 'obs-par', 9: 'obs-ev',
          5: 'obs-store', 6: 'dones+store'}
 
 
@@ -34,20 +34,24 @@ def main():
     st = torch.zeros((E, 16), dtype=torch.int64, device=eng.device)
     L.gw_debug_set_stamps(eng.h, C.c_void_p(st.data_ptr()))
     eng.reset()
-    order = [0, 1, 2, 3, 4, 8, 9, 5, 6]
+    order = [0, 10, 1, 2, 3, 4, 8, 9, 5, 6]
     deltas = []
     ends = []
+    resets = []
     for t in range(200):
         eng.random_actions(7, t)
         st.zero_()
-        eng.step()
+        eng.step_autoreset(horizon=200)
         torch.cuda.synchronize()
         s = st.cpu().numpy()
         if t >= 20:
             d = np.stack([s[:, order[i + 1]] - s[:, order[i]] for i in range(len(order) - 1)], 1)
             deltas.append(d)
-            ends.append(s[:, 6] - s[:, 0].min())
-        eng.reset(all_done=eng.all_done, horizon=200)
+            ends.append(s[:, 6] - s[:, 0])
+            rs = s[s[:, 12] != 0]
+            if len(rs):
+                resets.append(np.stack([rs[:, 10] - rs[:, 0], rs[:, 13] - rs[:, 12],
+                                        rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0]], 1))
     d = np.concatenate(deltas)
     tot = d.sum(1)
     print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
@@ -56,7 +60,14 @@ def main():
         print(f"  {NAMES[order[i]]:>8s} -> {NAMES[order[i+1]]:<12s} median {np.median(d[:, i]):8.0f}"
               f"  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum() * 100:5.1f}%")
     e = np.concatenate(ends)
-    print(f"env end time since first start: median {np.median(e):.0f} max {e.max()}")
+    print(f"whole env (stamp 0 -> 6): median {np.median(e):.0f} p99 {np.percentile(e, 99):.0f} "
+          f"max {e.max()}")
+    print(f"load (lanes+rng+actions, 0->10) median {np.median(d[:, 0] * 0 + (np.concatenate(deltas)[:, 0])):.0f}")
+    if resets:
+        r = np.concatenate(resets)
+        print(f"reset envs: {len(r)}; median cycles: load {np.median(r[:, 0]):.0f}, do_reset "
+              f"{np.median(r[:, 1]):.0f}, reset tables+obs {np.median(r[:, 2]):.0f}, whole env "
+              f"{np.median(r[:, 3]):.0f} (max {r[:, 3].max()})")
 
 
 if __name__ == '__main__':
