@@ -13,6 +13,16 @@ INCLUDE = os.path.join(os.path.dirname(PKG), 'include', 'gw_engine.h')
 LIB = os.path.join(PKG, '_build', 'libgw_engine.so')
 # diagnostic build with in-kernel s_memtime stamps (tools/stamps.py); never the default
 LIB_STAMPS = os.path.join(PKG, '_build', 'libgw_engine_stamps.so')
+# diagnostic build with bounds / one-lane checks that record instead of faulting
+LIB_CHECKS = os.path.join(PKG, '_build', 'libgw_engine_checks.so')
+VARIANT = os.environ.get('GW_ENGINE_VARIANT', '')   # '', 'stamps' or 'checks'
+if os.environ.get('GW_ENGINE_STAMPS') == '1':
+    VARIANT = 'stamps'
+
+
+def variant_lib(variant=None):
+    v = VARIANT if variant is None else variant
+    return {'': LIB, 'stamps': LIB_STAMPS, 'checks': LIB_CHECKS}[v]
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('GW_OFFLOAD_ARCH', 'gfx950')
 
@@ -35,9 +45,9 @@ SIGNATURES = {
 }
 
 
-def build(force=False, verbose=False, stamps=False):
+def build(force=False, verbose=False, stamps=False, checks=False):
     """Compile the engine for gfx950 with hipcc (works without a GPU)."""
-    out = LIB_STAMPS if stamps else LIB
+    out = LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB)
     deps = [SRC, INCLUDE]
     if not force and os.path.exists(out) and \
             os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
@@ -45,6 +55,7 @@ def build(force=False, verbose=False, stamps=False):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off',
            '-fPIC', '-shared', '-Wno-unused-result'] + (['-DGW_STAMPS'] if stamps else []) + \
+        (['-DGW_CHECKS'] if checks else []) + \
         ['-o', out + '.tmp', SRC]
     if verbose:
         print(' '.join(cmd))
@@ -60,11 +71,10 @@ def lib():
     """The loaded engine library; raises if it is missing (no fallback)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_STAMPS if os.environ.get('GW_ENGINE_STAMPS') == '1' else LIB):
+        if not os.path.exists(variant_lib()):
             raise RuntimeError(f"HIP engine library {LIB} is missing; run "
                                "`python -c 'import __graft_entry__ as g; g.build()'`")
-        path = LIB_STAMPS if os.environ.get('GW_ENGINE_STAMPS') == '1' else LIB
-        L = C.CDLL(path)
+        L = C.CDLL(variant_lib())
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -74,6 +74,7 @@ struct Params {
     uint64_t* acting; uint32_t* err;
     const uint8_t* mask; const uint8_t* prev_all_done; int32_t horizon; int32_t autoreset;
     uint64_t* stamps;   // diagnostic build only (-DGW_STAMPS): [E][16] s_memtime
+    uint32_t* dbg;      // diagnostic build only (-DGW_CHECKS): [16] first violation
     // config
     int32_t E, A, H, W, max_enc, sim_kind, nav, target;
     int32_t observe_self, stacked, no_overlap_at_reset, state_order;
@@ -112,6 +113,29 @@ __device__ __forceinline__ double rld(double v, int l)
 }
 
 __device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
+
+// ------------------------------------------------------------ checked build
+// -DGW_CHECKS: every data-dependent LDS index and every "exactly one lane"
+// ballot is validated; a violation is recorded in p.dbg and the access is
+// redirected to index 0 (the build cannot fault).  Never the shipped build.
+#ifdef GW_CHECKS
+__device__ __noinline__ void chk_fail(uint32_t* dbg, int code, int v0, int v1)
+{
+    if (!dbg) return;
+    if (atomicOr(&dbg[0], 1u << code) == 0u) {
+        dbg[1] = (uint32_t)code; dbg[2] = (uint32_t)v0; dbg[3] = (uint32_t)v1;
+        dbg[4] = blockIdx.x; dbg[5] = (uint32_t)__lane_id();
+    } else {
+        atomicAdd(&dbg[6], 1u);
+    }
+}
+#define CIDX(idx, lim, code) \
+    ([&](int _i, int _l) { if (_i < 0 || _i >= _l) { chk_fail(p.dbg, (code), _i, _l); return 0; } return _i; }((idx), (lim)))
+#define CHECK(cond, code, v0, v1) do { if (!(cond)) chk_fail(p.dbg, (code), (v0), (v1)); } while (0)
+#else
+#define CIDX(idx, lim, code) (idx)
+#define CHECK(cond, code, v0, v1) do { } while (0)
+#endif
 
 // DPP (GFX9 row_shr / row_bcast) wave primitives; call in uniform control flow
 template <int CTRL, int ROWMASK = 0xf>
@@ -293,6 +317,7 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
 __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L, bool valid)
 {
     if (!valid) return;
+    CHECK(!L.in_grid || (L.r >= 0 && L.r < p.H && L.c >= 0 && L.c < p.W), 12, L.r, L.c);
     size_t k = (size_t)e * p.A + lane_id();
     p.pos[k] = make_int2(L.r, L.c);
     p.seq[k] = L.seq;
@@ -352,12 +377,19 @@ __device__ __forceinline__ Smem carve(char* base, const Params& p)
 
 __device__ __forceinline__ int tbl_idx(const Params& p, int r, int c)
 {
-    return (r + p.pad) * p.pitch + (c + p.pad);
+    return CIDX((r + p.pad) * p.pitch + (c + p.pad), p.tbl_rows * p.pitch, 1);
 }
 
-__device__ __forceinline__ uint32_t cnt_get(const uint32_t* cnt, int cell)
+// index of `cell`'s packed count word
+__device__ __forceinline__ int cnt_word(const Params& p, int cell)
 {
-    return (cnt[cell >> 2] >> (8 * (cell & 3))) & 0xffu;
+    return CIDX(cell, p.H * p.W, 3) >> 2;
+}
+
+#define cnt_get(cnt, cell) cnt_get_((cnt), (cell), p)
+__device__ __forceinline__ uint32_t cnt_get_(const uint32_t* cnt, int cell, const Params& p)
+{
+    return (cnt[CIDX(cell, p.H * p.W, 4) >> 2] >> (8 * (cell & 3))) & 0xffu;
 }
 
 __device__ __forceinline__ uint8_t cell_byte(uint32_t count, int enc)
@@ -391,7 +423,7 @@ __device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, cons
 }
 
 // Build the padded byte table and the counts from the lanes' positions.
-__device__ void build_tables(const Params& p, Smem& sm, const Lane& L)
+__device__ __forceinline__ void build_tables(const Params& p, Smem& sm, const Lane& L)
 {
     const int l = lane_id();
     const int HW = p.H * p.W;
@@ -402,7 +434,7 @@ __device__ void build_tables(const Params& p, Smem& sm, const Lane& L)
     for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
     wave_sync();
     int cell = L.r * p.W + L.c;
-    if (L.in_grid) atomicAdd(&sm.cnt[cell >> 2], 1u << (8 * (cell & 3)));
+    if (L.in_grid) atomicAdd(&sm.cnt[cnt_word(p, cell)], 1u << (8 * (cell & 3)));
     wave_sync();
     if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, cell), L.enc);
     wave_sync();
@@ -413,12 +445,13 @@ __device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const La
 {
     const int l = lane_id();
     const int cell = r * p.W + c;
-    if (l == b) atomicSub(&sm.cnt[cell >> 2], 1u << (8 * (cell & 3)));
+    if (l == b) atomicSub(&sm.cnt[cnt_word(p, cell)], 1u << (8 * (cell & 3)));
     wave_sync();
     const uint32_t n = cnt_get(sm.cnt, cell);
     int enc = 0;
     if (n == 1) {
         const uint64_t m = __ballot(L.in_grid && L.r == r && L.c == c);
+        CHECK(__popcll(m) == 1, 10, r * 1000 + c, (int)n);
         enc = rl(L.enc, first_lane(m));
     }
     if (l == 0) sm.tbl[tbl_idx(p, r, c)] = cell_byte(n, enc);
@@ -428,7 +461,7 @@ __device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const La
 // ------------------------------------------------------------ observation
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S>
-__device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L)
+__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L)
 {
     constexpr int SS = S * S;
     constexpr int R = S / 2;
@@ -449,7 +482,8 @@ __device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const La
             for (int wr = 0; wr < S; wr++) {
                 const int o = o0 + wr * p.pitch;
 #pragma unroll
-                for (int d = 0; d < ND; d++) rows[wr][d] = t32[(o >> 2) + d];
+                for (int d = 0; d < ND; d++)
+                    rows[wr][d] = t32[CIDX((o >> 2) + d, (p.tbl_rows * p.pitch + 3) / 4, 2)];
             }
             const int sh = o0 & 3;
 #pragma unroll
@@ -496,6 +530,7 @@ __device__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const La
                 const bool mem = l < A && L.in_grid && L.r == gr && L.c == gc && (p.observe_self || l != o);
                 const uint64_t mm = __ballot(mem);
                 const int n = __popcll(mm);
+                CHECK(n >= 1, 11, gr * 1000 + gc, o);
                 const uint32_t j = rng.interval((uint32_t)(n - 1));
                 // the j-th member in insertion (seq) order
                 int sel = first_lane(mm);
@@ -580,7 +615,9 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     int rank = -1;                                         // rank among accepted
     int n = 0;
     for (int r = 0; r < ncand; r++) {
-        const int j = first_lane(__ballot(crank == r));
+        const uint64_t jm = __ballot(crank == r);
+        CHECK(__popcll(jm) == 1, 8, r, ncand);
+        const int j = first_lane(jm);
         const double u = rng.uniform();                     // _basic_criteria draw
         if (u > acc) continue;
         if (l == j) rank = n;
@@ -611,7 +648,9 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     }
     for (int t = 0; t < nlist; t++) {
         const int pr = rl(pick, t);
-        const int lane_t = first_lane(__ballot(rank == pr));
+        const uint64_t tm = __ballot(rank == pr);
+        CHECK(__popcll(tm) == 1, 9, pr, n);
+        const int lane_t = first_lane(tm);
         if (l == t) list = lane_t;
     }
     // apply damage in list order (actor.py:353-358)
@@ -670,7 +709,7 @@ __device__ __forceinline__ void renorm_seq(const Params& p, Lane& L, uint32_t& c
 // AllStepManager.reset (all_step_manager.py:37-49) -> SmartGWS.reset ->
 // PositionState.reset (state.py:88-166) / HealthState.reset (:629-641) in the
 // pinned order.  Returns false on the reference's placement exceptions.
-__device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr, uint32_t& err)
+__device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr, uint32_t& err)
 {
     const int l = lane_id();
     const int A = p.A;
@@ -698,7 +737,7 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
                     uint32_t w[2];
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
-                        uint32_t y = rng.key[rng.pos + 2 * k + q];
+                        uint32_t y = rng.key[CIDX(rng.pos + 2 * k + q, GW_MT_N, 5)];
                         y ^= (y >> 11);
                         y ^= (y << 7) & 0x9d2c5680u;
                         y ^= (y << 15) & 0xefc60000u;
@@ -774,7 +813,10 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
                     const bool mine = pc != 0 && excl <= idx && idx < inc;
                     int c0 = 0;
                     if (mine) c0 = l * 64 + select_bit(w, idx - excl);
-                    cell = rl(c0, first_lane(__ballot(mine)));
+                    const uint64_t mm = __ballot(mine);
+                    CHECK(__popcll(mm) == 1, 6, (int)idx, (int)tot);
+                    cell = rl(c0, first_lane(mm));
+                    CHECK(cell >= 0 && cell < HW, 7, cell, a);
                     // cells from the availability list always pass Grid.query
                 }
                 const int r = cell / p.W, c = cell % p.W;
@@ -869,7 +911,7 @@ __device__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t&
 }
 
 template <int S>
-__device__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr)
+__device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr)
 {
     constexpr int SS = S * S;
     uint32_t err = 0;
@@ -959,8 +1001,8 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         wave_sync();
         const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
         if (real) {
-            atomicAdd(&sm.tcnt[tgt >> 2], 1u << (8 * (tgt & 3)));
-            atomicAdd(&sm.scnt[src >> 2], 1u << (8 * (src & 3)));
+            atomicAdd(&sm.tcnt[cnt_word(p, tgt)], 1u << (8 * (tgt & 3)));
+            atomicAdd(&sm.scnt[cnt_word(p, src)], 1u << (8 * (src & 3)));
         }
         wave_sync();
         bool iso = false, iso_ok = false;
@@ -986,8 +1028,8 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         wave_sync();
         if (moved) {
             const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
-            atomicSub(&sm.cnt[oc >> 2], 1u << (8 * (oc & 3)));
-            atomicAdd(&sm.cnt[ncl >> 2], 1u << (8 * (ncl & 3)));
+            atomicSub(&sm.cnt[cnt_word(p, oc)], 1u << (8 * (oc & 3)));
+            atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
             sm.tbl[tbl_idx(p, pr, pc)] = 0;
         }
         wave_sync();
@@ -1007,7 +1049,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
             if (ok && (qr != pr || qc != pc)) {
                 table_remove(p, sm, L, n, pr, pc);
                 const int ncl = qr * p.W + qc;
-                if (l == n) atomicAdd(&sm.cnt[ncl >> 2], 1u << (8 * (ncl & 3)));
+                if (l == n) atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
                 wave_sync();
                 if (L.in_grid && L.r == qr && L.c == qc)
                     sm.tbl[tbl_idx(p, qr, qc)] = cell_byte(cnt_get(sm.cnt, ncl), L.enc);
@@ -1422,6 +1464,14 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     if (seq) HIPCHK(hipMemcpyAsync(g->base.seq, seq, EA * 4, hipMemcpyDeviceToDevice, st));
     if (mt) HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
     if (steps) HIPCHK(hipMemcpyAsync(g->base.steps, steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
+// diagnostic hook (not in the public header): violation record for -DGW_CHECKS builds
+gw_status gw_debug_set_checks(gw_handle g, uint32_t* dbg)
+{
+    if (!g) return GW_E_INVALID;
+    g->base.dbg = dbg;
     return GW_OK;
 }
 

@@ -52,7 +52,21 @@ class GridWorldEngine:
         self.err = torch.zeros((E,), dtype=torch.int32, device=dev)
         self.acting = torch.zeros((E,), dtype=torch.int64, device=dev)
         self.actions = torch.zeros((E, A, _abi.GW_ACT_DIM), dtype=torch.int32, device=dev)
+        self._dbg = None
+        if _native.VARIANT == 'checks':
+            self._dbg = torch.zeros(16, dtype=torch.int32, device=dev)
+            self.L.gw_debug_set_checks.argtypes = [C.c_void_p, C.c_void_p]
+            self.L.gw_debug_set_checks(self.h, _ptr(self._dbg))
         self.seed(env_seeds(E) if seeds is None else seeds)
+
+    def _check_debug(self, what):
+        if self._dbg is None:
+            return
+        d = self._dbg.cpu().numpy().view(np.uint32)
+        if d[0]:
+            raise AssertionError(
+                f"GW_CHECKS violation after {what}: mask={d[0]:#x} first code={d[1]} v0={int(np.int32(d[2]))} "
+                f"v1={int(np.int32(d[3]))} env={d[4]} lane={d[5]} more={d[6]}")
 
     def __del__(self):
         h = getattr(self, 'h', None)
@@ -79,6 +93,7 @@ class GridWorldEngine:
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_reset(self.h, _ptr(mask), _ptr(all_done), int(horizon),
                                           _ptr(out), _ptr(self.err), _stream()), 'gw_reset')
+        self._check_debug('gw_reset')
         return out
 
     def step(self, actions=None):
@@ -89,6 +104,7 @@ class GridWorldEngine:
             _native.check(self.L.gw_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
                                          _ptr(self.done), _ptr(self.all_done), _ptr(self.acting),
                                          _stream()), 'gw_step')
+        self._check_debug('gw_step')
         return self.obs, self.reward, self.done, self.all_done
 
     def step_autoreset(self, actions=None, horizon=0):
@@ -102,6 +118,7 @@ class GridWorldEngine:
                 self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
                 _ptr(self.all_done), _ptr(self.acting), int(horizon), _ptr(self.err), _stream()),
                 'gw_step_autoreset')
+        self._check_debug('gw_step_autoreset')
         return self.obs, self.reward, self.done, self.all_done
 
     def random_actions(self, key, step, env_offset=0, out=None):
