@@ -331,8 +331,7 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
 //                           0x80 >= 2 occupants, 0xFF off-grid (border)
 //   cnt  [ceil(HW/4)] u32   per-cell occupant counts, packed u8
 //   work union: { tcnt, scnt [2][ceil(HW/4)] u32 (move isolation)
-//               | stage [A*SS] i8 (observations)
-//               | avail [(max_enc+1)*64] u64 (reset availability bitmaps) }
+//               | stage [A*SS] i8 (observations) }
 struct Smem {
     uint32_t* key;
     uint8_t* tbl;
@@ -340,7 +339,6 @@ struct Smem {
     uint32_t* tcnt;
     uint32_t* scnt;
     int8_t* stage;
-    uint64_t* avail;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -349,10 +347,8 @@ __host__ __device__ inline size_t work_bytes(int HW, int A, int SS, int max_enc)
 {
     size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
     size_t s = align16((size_t)A * SS);
-    size_t v = align16((size_t)(max_enc + 1) * 64 * 8);
-    if (s > w) w = s;
-    if (v > w) w = v;
-    return w;
+    (void)max_enc;
+    return s > w ? s : w;
 }
 
 __host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, int tbl_bytes)
@@ -371,7 +367,6 @@ __device__ __forceinline__ Smem carve(char* base, const Params& p)
     s.tcnt = (uint32_t*)base;
     s.scnt = (uint32_t*)(base + align16((size_t)((HW + 3) / 4) * 4));
     s.stage = (int8_t*)base;
-    s.avail = (uint64_t*)base;
     return s;
 }
 
@@ -765,146 +760,81 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         }
     };
 
-    // PositionState with <= 4 encodings: the availability bitmaps live in
-    // registers (lane w holds word w), with each lane's inclusive prefix
-    // popcount and the per-encoding totals maintained incrementally, so a
-    // placement is one draw, one ballot and a handful of lane-local updates.
-    constexpr int ME = 4;
-    auto position_reset_regs = [&]() -> bool {
-        const int nwords = (HW + 63) / 64;
-        uint64_t av[ME + 1];
-        uint32_t pcnt[ME + 1], incl[ME + 1], total[ME + 1];
-        uint64_t full = 0;
-        if (l < nwords) {
-            const int rem = HW - l * 64;
-            full = rem >= 64 ? ~0ull : ((1ull << rem) - 1);
-        }
-        const uint32_t fpc = (uint32_t)__popcll(full);
-        const uint32_t fincl = wave_incl_scan(fpc);
-#pragma unroll
-        for (int f = 0; f <= ME; f++) {
-            av[f] = (f >= 1 && f <= p.max_enc) ? full : 0ull;
-            pcnt[f] = (f >= 1 && f <= p.max_enc) ? fpc : 0u;
-            incl[f] = (f >= 1 && f <= p.max_enc) ? fincl : 0u;
-            total[f] = (f >= 1 && f <= p.max_enc) ? (uint32_t)HW : 0u;
-        }
+    // PositionState (state.py:88-166) without availability bitmaps: list e
+    // is "every cell except the distinct cells removed from it", and the
+    // removed cells are the placed lanes' own cells.  Lane j carries its
+    // cell and remeff_j = the lists its placement removed a NEW cell from
+    // (a cell already removed is not counted twice, as list.remove raising
+    // ValueError in the reference).  The idx-th listed cell is the least
+    // fixpoint of c = idx + #{removed cells <= c}; list lengths are one
+    // register, lane e holding |list e|.
+    auto position_reset_lanes = [&]() -> bool {
+        int cell_l = -1;                 // this lane's cell once placed
+        uint32_t remeff = 0;             // lists this lane's placement shortened
+        uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)HW : 0u;
+        const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         for (int pass = 0; pass < 2; pass++) {
             for (int a = 0; a < A; a++) {
-                const int ir = rl(L.init_r, a), ic = rl(L.init_c, a);
+                const int ir = rl(L.init_r, a);
                 const bool has_ip = ir >= 0;
                 if ((pass == 0) != has_ip) continue;
                 const int aenc = rl(L.enc, a);
                 const uint32_t aov = rl(L.ov, a);
                 int cell;
                 if (has_ip) {
+                    const int ic = rl(L.init_c, a);
                     cell = ir * p.W + ic;
-                    // Grid.place -> query (grid.py:81-129); asserted by the reference
-                    const bool blocks = valid && L.in_grid && L.r == ir && L.c == ic &&
-                                        !((aov >> L.enc) & 1u);
+                    // Grid.place -> query (grid.py:81-129), asserted by the reference
+                    const bool blocks = valid && L.in_grid && cell_l == cell && !((aov >> L.enc) & 1u);
                     if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
                 } else {
-                    uint64_t w = 0; uint32_t pc = 0, inc = 0, tot = 0;
-#pragma unroll
-                    for (int f = 1; f <= ME; f++)
-                        if (aenc == f) { w = av[f]; pc = pcnt[f]; inc = incl[f]; tot = total[f]; }
-                    if (tot == 0) { err |= GW_ERR_NO_CELL; return false; }
-                    const uint32_t idx = rng.interval(tot - 1);   // np.random.choice(list, 1)
-                    const uint32_t excl = inc - pc;
-                    const bool mine = pc != 0 && excl <= idx && idx < inc;
-                    int c0 = 0;
-                    if (mine) c0 = l * 64 + select_bit(w, idx - excl);
-                    const uint64_t mm = __ballot(mine);
-                    CHECK(__popcll(mm) == 1, 6, (int)idx, (int)tot);
-                    cell = rl(c0, first_lane(mm));
-                    CHECK(cell >= 0 && cell < HW, 7, cell, a);
-                    // cells from the availability list always pass Grid.query
-                }
-                const int r = cell / p.W, c = cell % p.W;
-                if (l == a) { L.r = r; L.c = c; L.in_grid = true; L.seq = ctr; }
-                ctr++;
-                // _update_available_positions (state.py:126-141)
-                const int wl = cell >> 6;
-                const uint64_t bit = 1ull << (cell & 63);
-#pragma unroll
-                for (int f = 1; f <= ME; f++) {
-                    if (f > p.max_enc) continue;
-                    if (!(p.no_overlap_at_reset || !((aov >> f) & 1u))) continue;
-                    const bool was = l == wl && (av[f] & bit) != 0;
-                    if (__ballot(was)) {                         // cell still listed
-                        if (l == wl) { av[f] &= ~bit; pcnt[f] -= 1; }
-                        if (l >= wl) incl[f] -= 1;
-                        total[f] -= 1;
+                    const uint32_t n = rl(lens, aenc);
+                    if (n == 0) { err |= GW_ERR_NO_CELL; return false; }
+                    const uint32_t idx = rng.interval(uni(n - 1));   // np.random.choice(list, 1)
+                    const bool inlist = L.in_grid && ((remeff >> aenc) & 1u);
+                    int c = (int)idx;
+                    for (;;) {
+                        const int c2 = (int)idx + __popcll(__ballot(inlist && cell_l <= c));
+                        if (c2 == c) break;
+                        c = c2;
                     }
+                    cell = uni(c);
+                    CHECK(cell >= 0 && cell < HW, 7, cell, a);
+                    // a cell taken from list aenc always passes Grid.query
                 }
-            }
-        }
-        return true;
-    };
-
-    auto position_reset = [&]() -> bool {
-        // availability lists -> bitmaps (the lists stay in ascending cell
-        // order under list.remove); lane w holds word w of each bitmap
-        const int nwords = (HW + 63) / 64;
-        for (int enc = 1; enc <= p.max_enc; enc++) {
-            uint64_t w = 0;
-            if (l < nwords) {
-                int rem = HW - l * 64;
-                w = rem >= 64 ? ~0ull : ((1ull << rem) - 1);
-            }
-            sm.avail[enc * 64 + l] = w;
-        }
-        wave_sync();
-        for (int pass = 0; pass < 2; pass++) {
-            for (int a = 0; a < A; a++) {
-                const int ir = rl(L.init_r, a), ic = rl(L.init_c, a);
-                const bool has_ip = ir >= 0;
-                if ((pass == 0) != has_ip) continue;
-                const int aenc = rl(L.enc, a);
-                int r, c;
-                if (has_ip) { r = ir; c = ic; }
-                else {
-                    const uint64_t w = (l < nwords) ? sm.avail[aenc * 64 + l] : 0ull;
-                    const uint32_t pc = (uint32_t)__popcll(w);
-                    const uint32_t incl = wave_incl_scan(pc);
-                    const uint32_t total = rl(incl, WAVE - 1);
-                    if (total == 0) { err |= GW_ERR_NO_CELL; return false; }
-                    const uint32_t idx = rng.interval(total - 1);
-                    const uint32_t excl = incl - pc;
-                    const bool mine = pc != 0 && excl <= idx && idx < incl;
-                    int cell = 0;
-                    if (mine) cell = l * 64 + select_bit(w, idx - excl);
-                    cell = rl(cell, first_lane(__ballot(mine)));
-                    r = cell / p.W; c = cell % p.W;
-                }
-                // Grid.place -> query (grid.py:81-129)
-                const uint32_t aov = rl(L.ov, a);
-                const bool blocks = valid && L.in_grid && L.r == r && L.c == c && !((aov >> L.enc) & 1u);
-                if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
-                if (l == a) { L.r = r; L.c = c; L.in_grid = true; L.seq = ctr; }
-                ctr++;
                 // _update_available_positions (state.py:126-141)
-                const int cell = r * p.W + c;
-                if (l == (cell >> 6)) {
-                    for (int enc = 1; enc <= p.max_enc; enc++)
-                        if (p.no_overlap_at_reset || !((aov >> enc) & 1u))
-                            sm.avail[enc * 64 + l] &= ~(1ull << (cell & 63));
+                const uint32_t rem = p.no_overlap_at_reset ? all_encs : (all_encs & ~aov);
+                uint32_t fresh = 0;
+                for (uint32_t m = rem; m; m &= m - 1) {
+                    const int f = __builtin_ctz(m);
+                    if (!__ballot(L.in_grid && cell_l == cell && ((remeff >> f) & 1u))) fresh |= 1u << f;
                 }
-                wave_sync();
+                if (l >= 1 && l <= p.max_enc && ((fresh >> l) & 1u)) lens -= 1;
+                if (l == a) {
+                    cell_l = cell; remeff = fresh; L.in_grid = true; L.seq = ctr;
+                }
+                ctr++;
             }
         }
+        if (L.in_grid) { L.r = cell_l / p.W; L.c = cell_l % p.W; }
         return true;
     };
 
-    auto place = [&]() -> bool {
-        return p.max_enc <= ME ? position_reset_regs() : position_reset();
-    };
+    auto place = [&]() -> bool { return position_reset_lanes(); };
+#ifdef GW_STAMPS
+    const int e = blockIdx.x;
+#endif
     bool ok;
     if (p.state_order == GW_ORDER_POSITION_HEALTH) {
         ok = place();
+        STAMP(11);
         if (ok && has_health) health_reset();
+        STAMP(15);
     } else {
         if (has_health) health_reset();
+        STAMP(11);
         ok = place();
+        STAMP(15);
     }
     if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
     return ok;

@@ -25,6 +25,9 @@ NAMES = {0: 'start', 1: 'tables', 10: 'load', 2: 'attack', 3: 'move', 4: 'cells'
          5: 'obs-store', 6: 'dones+store'}
 
 
+HORIZON = int(os.environ.get('HORIZON', '100000'))
+
+
 def main():
     cc = bench.team_battle_sim().compiled()
     E = int(os.environ.get('ENVS', '4096'))
@@ -38,12 +41,20 @@ def main():
     deltas = []
     ends = []
     resets = []
-    for t in range(200):
+    kms, span, emax = [], [], []
+    for t in range(int(os.environ.get('STEPS', '300'))):
         eng.random_actions(7, t)
         st.zero_()
-        eng.step_autoreset(horizon=200)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        eng.step_autoreset(horizon=HORIZON)
+        ev1.record()
         torch.cuda.synchronize()
         s = st.cpu().numpy()
+        if t >= 20:
+            kms.append(ev0.elapsed_time(ev1))
+            span.append(int(s[:, 6].max() - s[:, 0].min()))
+            emax.append(int((s[:, 6] - s[:, 0]).max()))
         if t >= 20:
             d = np.stack([s[:, order[i + 1]] - s[:, order[i]] for i in range(len(order) - 1)], 1)
             deltas.append(d)
@@ -51,7 +62,8 @@ def main():
             rs = s[s[:, 12] != 0]
             if len(rs):
                 resets.append(np.stack([rs[:, 10] - rs[:, 0], rs[:, 13] - rs[:, 12],
-                                        rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0]], 1))
+                                        rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0],
+                                        rs[:, 11] - rs[:, 12], rs[:, 15] - rs[:, 11]], 1))
     d = np.concatenate(deltas)
     tot = d.sum(1)
     print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
@@ -59,6 +71,9 @@ def main():
     for i in range(len(order) - 1):
         print(f"  {NAMES[order[i]]:>8s} -> {NAMES[order[i+1]]:<12s} median {np.median(d[:, i]):8.0f}"
               f"  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum() * 100:5.1f}%")
+    print(f"kernel ms (events) mean {np.mean(kms):.4f}; stamp span (last end - first start) mean "
+          f"{np.mean(span):.0f} ticks -> {np.mean(span) / np.mean(kms) / 1e6:.3f} ticks/ns; "
+          f"max env duration mean {np.mean(emax):.0f} ticks")
     e = np.concatenate(ends)
     print(f"whole env (stamp 0 -> 6): median {np.median(e):.0f} p99 {np.percentile(e, 99):.0f} "
           f"max {e.max()}")
@@ -67,7 +82,8 @@ def main():
         r = np.concatenate(resets)
         print(f"reset envs: {len(r)}; median cycles: load {np.median(r[:, 0]):.0f}, do_reset "
               f"{np.median(r[:, 1]):.0f}, reset tables+obs {np.median(r[:, 2]):.0f}, whole env "
-              f"{np.median(r[:, 3]):.0f} (max {r[:, 3].max()})")
+              f"{np.median(r[:, 3]):.0f} (max {r[:, 3].max()}); placement {np.median(r[:, 4]):.0f}, "
+              f"health {np.median(r[:, 5]):.0f}")
 
 
 if __name__ == '__main__':
