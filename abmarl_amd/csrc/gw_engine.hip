@@ -73,7 +73,7 @@ struct Params {
     const int32_t* actions; int32_t* obs; double* reward; uint8_t* done; uint8_t* all_done;
     uint64_t* acting; uint32_t* err;
     const uint8_t* mask; const uint8_t* prev_all_done; int32_t horizon; int32_t autoreset;
-    uint64_t* stamps;   // diagnostic build only (-DGW_STAMPS): [E][16] s_memtime
+    uint64_t* stamps;   // diagnostic build only (-DGW_STAMPS): [E][32] s_memtime
     uint32_t* dbg;      // diagnostic build only (-DGW_CHECKS): [16] first violation
     // config
     int32_t E, A, H, W, max_enc, sim_kind, nav, target;
@@ -188,7 +188,7 @@ __device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
     do {                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                        \
         uint64_t _t = __builtin_amdgcn_s_memtime();                               \
-        if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * 16 + (i)] = _t;      \
+        if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * 32 + (i)] = _t;      \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
 #else
@@ -768,6 +768,12 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     // ValueError in the reference).  The idx-th listed cell is the least
     // fixpoint of c = idx + #{removed cells <= c}; list lengths are one
     // register, lane e holding |list e|.
+#ifdef GW_STAMPS
+    uint64_t acc_t[5] = {0, 0, 0, 0, 0};
+#define ACC_T(k, t0) do { __builtin_amdgcn_sched_barrier(0); uint64_t _n = __builtin_amdgcn_s_memtime(); acc_t[k] += _n - (t0); t0 = _n; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define ACC_T(k, t0) do { } while (0)
+#endif
     auto position_reset_lanes = [&]() -> bool {
         int cell_l = -1;                 // this lane's cell once placed
         uint32_t remeff = 0;             // lists this lane's placement shortened
@@ -775,12 +781,16 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         for (int pass = 0; pass < 2; pass++) {
             for (int a = 0; a < A; a++) {
+#ifdef GW_STAMPS
+                uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
                 const int ir = rl(L.init_r, a);
                 const bool has_ip = ir >= 0;
                 if ((pass == 0) != has_ip) continue;
                 const int aenc = rl(L.enc, a);
                 const uint32_t aov = rl(L.ov, a);
                 int cell;
+                ACC_T(0, t0);
                 if (has_ip) {
                     const int ic = rl(L.init_c, a);
                     cell = ir * p.W + ic;
@@ -791,6 +801,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     const uint32_t n = rl(lens, aenc);
                     if (n == 0) { err |= GW_ERR_NO_CELL; return false; }
                     const uint32_t idx = rng.interval(uni(n - 1));   // np.random.choice(list, 1)
+                    ACC_T(1, t0);
                     const bool inlist = L.in_grid && ((remeff >> aenc) & 1u);
                     int c = (int)idx;
                     for (;;) {
@@ -801,6 +812,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     cell = uni(c);
                     CHECK(cell >= 0 && cell < HW, 7, cell, a);
                     // a cell taken from list aenc always passes Grid.query
+                    ACC_T(2, t0);
                 }
                 // _update_available_positions (state.py:126-141)
                 const uint32_t rem = p.no_overlap_at_reset ? all_encs : (all_encs & ~aov);
@@ -814,9 +826,14 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     cell_l = cell; remeff = fresh; L.in_grid = true; L.seq = ctr;
                 }
                 ctr++;
+                ACC_T(3, t0);
             }
         }
         if (L.in_grid) { L.r = cell_l / p.W; L.c = cell_l % p.W; }
+#ifdef GW_STAMPS
+        if (l == 0 && p.stamps)
+            for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * 32 + 16 + k] = acc_t[k];
+#endif
         return true;
     };
 

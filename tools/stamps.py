@@ -34,7 +34,7 @@ def main():
     eng = GridWorldEngine(cc, E, seeds=env_seeds(E))
     L = eng.L
     L.gw_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
-    st = torch.zeros((E, 16), dtype=torch.int64, device=eng.device)
+    st = torch.zeros((E, 32), dtype=torch.int64, device=eng.device)
     L.gw_debug_set_stamps(eng.h, C.c_void_p(st.data_ptr()))
     eng.reset()
     order = [0, 10, 1, 2, 3, 4, 8, 9, 5, 6]
@@ -63,7 +63,8 @@ def main():
             if len(rs):
                 resets.append(np.stack([rs[:, 10] - rs[:, 0], rs[:, 13] - rs[:, 12],
                                         rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0],
-                                        rs[:, 11] - rs[:, 12], rs[:, 15] - rs[:, 11]], 1))
+                                        rs[:, 11] - rs[:, 12], rs[:, 15] - rs[:, 11],
+                                        rs[:, 16], rs[:, 17], rs[:, 18], rs[:, 19]], 1))
     d = np.concatenate(deltas)
     tot = d.sum(1)
     print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
@@ -84,6 +85,8 @@ def main():
               f"{np.median(r[:, 1]):.0f}, reset tables+obs {np.median(r[:, 2]):.0f}, whole env "
               f"{np.median(r[:, 3]):.0f} (max {r[:, 3].max()}); placement {np.median(r[:, 4]):.0f}, "
               f"health {np.median(r[:, 5]):.0f}")
+        print(f"placement loop parts (median sums): head {np.median(r[:, 6]):.0f} draw "
+              f"{np.median(r[:, 7]):.0f} fixpoint {np.median(r[:, 8]):.0f} update {np.median(r[:, 9]):.0f}")
 
 
 if __name__ == '__main__':
