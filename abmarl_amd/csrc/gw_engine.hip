@@ -196,6 +196,43 @@ __device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
 #endif
 
 // ------------------------------------------------------------ MT19937
+__device__ __forceinline__ uint32_t temper(uint32_t y)
+{
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// mt19937.c mt19937_gen, lane-parallel in chunks of 64 (every write's
+// dependency i-227 is >= 3 chunks back; i+1 is read before any lane writes)
+__device__ __forceinline__ void mt_twist(uint32_t* key)
+{
+    const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
+    const int l = lane_id();
+    wave_sync();
+    for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
+        int i = b + l;
+        uint32_t nv = 0;
+        if (i < GW_MT_N - 1) {
+            uint32_t y = (key[i] & UP) | (key[i + 1] & LO);
+            int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
+            nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+        }
+        wave_sync();
+        if (i < GW_MT_N - 1) key[i] = nv;
+        wave_sync();
+    }
+    {
+        uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
+        uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+        wave_sync();
+        if (l == 0) key[GW_MT_N - 1] = nv;
+        wave_sync();
+    }
+}
+
 // numpy legacy RandomState (mt19937.c): key[] lives in LDS; tempered output
 // words are cached one per lane (a 64-word block), so a draw is one
 // v_readlane; the twist is lane-parallel in chunks of 64 (every write's
@@ -209,28 +246,7 @@ struct Rng {
 
     __device__ __forceinline__ void twist()
     {
-        const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
-        const int l = lane_id();
-        wave_sync();
-        for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
-            int i = b + l;
-            uint32_t nv = 0;
-            if (i < GW_MT_N - 1) {
-                uint32_t y = (key[i] & UP) | (key[i + 1] & LO);
-                int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
-                nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
-            }
-            wave_sync();
-            if (i < GW_MT_N - 1) key[i] = nv;
-            wave_sync();
-        }
-        {
-            uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
-            uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
-            wave_sync();
-            if (l == 0) key[GW_MT_N - 1] = nv;
-            wave_sync();
-        }
+        mt_twist(key);
         pos = 0;
         base = -1;
         dirty = true;
@@ -242,12 +258,7 @@ struct Rng {
         int b = pos & ~(WAVE - 1);
         if (b != base) {
             int i = b + lane_id();
-            uint32_t y = i < GW_MT_N ? key[i] : 0u;
-            y ^= (y >> 11);
-            y ^= (y << 7) & 0x9d2c5680u;
-            y ^= (y << 15) & 0xefc60000u;
-            y ^= (y >> 18);
-            cache = y;
+            cache = temper(i < GW_MT_N ? key[i] : 0u);
             base = b;
         }
         uint32_t v = rl(cache, pos & (WAVE - 1));
@@ -341,6 +352,10 @@ struct Smem {
     int8_t* stage;
 };
 
+// Jacobi placement scratch (do_reset): words [JAC_WB] u32 | pub [64] uint2 | key2 [624] u32
+constexpr int JAC_WB = 192;
+constexpr size_t JAC_WORK_BYTES = 4 * JAC_WB + 8 * 64 + 4 * GW_MT_N;
+
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 __host__ __device__ inline size_t work_bytes(int HW, int A, int SS, int max_enc)
@@ -348,7 +363,8 @@ __host__ __device__ inline size_t work_bytes(int HW, int A, int SS, int max_enc)
     size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
     size_t s = align16((size_t)A * SS);
     (void)max_enc;
-    return s > w ? s : w;
+    if (s < w) s = w;
+    return s > JAC_WORK_BYTES ? s : JAC_WORK_BYTES;
 }
 
 __host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, int tbl_bytes)
@@ -732,12 +748,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     uint32_t w[2];
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
-                        uint32_t y = rng.key[CIDX(rng.pos + 2 * k + q, GW_MT_N, 5)];
-                        y ^= (y >> 11);
-                        y ^= (y << 7) & 0x9d2c5680u;
-                        y ^= (y << 15) & 0xefc60000u;
-                        y ^= (y >> 18);
-                        w[q] = y;
+                        w[q] = temper(rng.key[CIDX(rng.pos + 2 * k + q, GW_MT_N, 5)]);
                     }
                     h = ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6)) / 9007199254740992.0;
                 }
@@ -837,7 +848,153 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         return true;
     };
 
-    auto place = [&]() -> bool { return position_reset_lanes(); };
+    // The same placement solved for all lanes at once: every unknown of the
+    // sequential loop above (|list|, the stream offset and index of the draw,
+    // the cell, which lists the cell was freshly removed from) is re-derived
+    // each sweep from the other lanes' current estimates, until a sweep
+    // changes nothing.  Lane i only depends on lanes placed before it, so the
+    // fixed point is the sequential result; the cell is checked to be the
+    // LEAST fixpoint of c = idx + #{removed <= c} (a larger one sits on a
+    // removed cell).  Returns 0 placed, 1 placement exception (err set),
+    // 2 unresolved (more than JAC_WB words / sweep cap): run the serial loop.
+    auto position_reset_jacobi = [&]() -> int {
+        constexpr int MAX_SWEEPS = 48;
+        const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
+        const bool ip = valid && L.init_r >= 0;
+        const bool rnd = valid && !ip;
+        const uint64_t ipm = __ballot(ip), rndm = __ballot(rnd);
+        const int nrnd = __popcll(rndm);
+        if (nrnd + 8 > JAC_WB) return 2;
+        const uint64_t lt = (1ull << l) - 1ull;
+        const uint32_t ord = valid ? (ip ? (uint32_t)l : 64u + (uint32_t)l) : 255u;
+        const uint64_t before = ip ? (ipm & lt) : (ipm | (rndm & lt));
+        const uint32_t rem = valid ? (p.no_overlap_at_reset ? all_encs : (all_encs & ~L.ov)) : 0u;
+        const uint32_t encbit = 1u << L.enc;
+        uint32_t* wbuf = (uint32_t*)sm.stage;
+        uint2* pub = (uint2*)(sm.stage + 4 * JAC_WB);
+        uint32_t* key2 = (uint32_t*)(sm.stage + 4 * JAC_WB + 8 * 64);
+        const int pos0 = rng.pos;
+        const bool crosses = pos0 + JAC_WB > GW_MT_N;
+        wave_sync();
+        if (nrnd > 0) {
+            // the next JAC_WB tempered words of the stream, across a twist
+            // into a copy of the key (the live key changes only if used)
+            for (int t = l; t < JAC_WB; t += WAVE) {
+                const int k = pos0 + t;
+                if (k < GW_MT_N) wbuf[t] = temper(rng.key[k]);
+            }
+            if (crosses) {
+                for (int i = l; i < GW_MT_N; i += WAVE) key2[i] = rng.key[i];
+                mt_twist(key2);
+                for (int t = l; t < JAC_WB; t += WAVE) {
+                    const int k = pos0 + t - GW_MT_N;
+                    if (k >= 0) wbuf[t] = temper(key2[k]);
+                }
+            }
+            wave_sync();
+        }
+        int cell = ip ? L.init_r * p.W + L.init_c : HW + l;   // distinct off-grid guesses
+        uint32_t fresh = rem;
+        int used = rnd ? 1 : 0;
+        int idx = -1;
+        uint32_t n = 0;
+        bool bad = false, qbad = false;
+        for (int sweep = 0;; sweep++) {
+            if (sweep == MAX_SWEEPS) return 2;
+            // |list enc| when this lane is placed
+            uint64_t mym = 0;
+            for (int f = 1; f <= p.max_enc; f++) {
+                const uint64_t m = __ballot((fresh >> f) & 1u);
+                if (L.enc == f) mym = m;
+            }
+            n = (uint32_t)HW - (uint32_t)__popcll(mym & before);
+            // interval(n - 1) draws: stream offsets = exclusive scan of words
+            // used; iterate until consistent (each pass fixes the first lane)
+            const bool draws = rnd && n > 1;
+            const uint32_t mx = n - 1u;
+            uint32_t mk = mx;
+            mk |= mk >> 1; mk |= mk >> 2; mk |= mk >> 4; mk |= mk >> 8; mk |= mk >> 16;
+            int nidx = 0;
+            for (int it = 0; it <= WAVE; it++) {
+                const int st = (int)(wave_incl_scan((uint32_t)used) - (uint32_t)used);
+                int nu = 0;
+                nidx = 0;
+                bad = false;
+                if (draws) {
+                    int q = st;
+                    for (;;) {
+                        if (q >= JAC_WB) { bad = true; break; }
+                        const uint32_t w = wbuf[CIDX(q, JAC_WB, 13)] & mk;
+                        q++;
+                        if (w <= mx) { nidx = (int)w; break; }
+                    }
+                    nu = q - st;
+                }
+                const bool ch = __ballot(nu != used) != 0;
+                used = nu;
+                if (!ch) break;
+            }
+            // cells: count removed cells <= the current estimate
+            if (valid) pub[l] = make_uint2((uint32_t)cell | (ord << 16) | ((uint32_t)L.enc << 24), fresh);
+            wave_sync();
+            const int ce = (nidx != idx) ? nidx : cell;
+            int cnt = 0;
+            bool inR = false, qb = false;
+            uint32_t dup = 0;
+#pragma unroll 4
+            for (int j = 0; j < A; j++) {
+                const uint2 q = pub[j];
+                const int cj = (int)(q.x & 0xffffu);
+                const bool bef = ((q.x >> 16) & 0xffu) < ord;
+                const bool rj = bef && (q.y & encbit);
+                cnt += (rj && cj <= ce) ? 1 : 0;
+                inR |= rj && cj == ce;
+                if (bef && cj == cell) {
+                    dup |= q.y;
+                    qb |= !((L.ov >> (q.x >> 24)) & 1u);
+                }
+            }
+            wave_sync();
+            int cn = cell;
+            if (rnd) {
+                cn = nidx + cnt;
+                if (inR && cn == ce) cn = nidx;   // a fixpoint on a removed cell is not the least
+            }
+            const uint32_t nf = rem & ~dup;
+            const bool lane_ch = valid && (cn != cell || nf != fresh || nidx != idx || (rnd && inR));
+            const bool any = __ballot(lane_ch) != 0;
+            cell = cn; fresh = nf; idx = nidx; qbad = qb;
+            if (!any) break;
+        }
+        if (__ballot(bad)) return 2;
+        if (__ballot(ip && qbad)) { err |= GW_ERR_INIT_POSITION; return 1; }   // grid.py:81-129
+        if (__ballot(rnd && n == 0)) return 2;   // the serial loop raises at the right point
+        const int total = (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
+        const int np = pos0 + total;
+        if (np > GW_MT_N) {   // the draws crossed the twist: the copy is the live key
+            for (int i = l; i < GW_MT_N; i += WAVE) rng.key[i] = key2[i];
+            wave_sync();
+            rng.pos = np - GW_MT_N;
+            rng.dirty = true;
+        } else {
+            rng.pos = np;
+        }
+        rng.base = -1;
+        CHECK(!valid || (cell >= 0 && cell < HW), 7, cell, l);
+        if (valid) {
+            L.in_grid = true;
+            L.r = cell / p.W; L.c = cell % p.W;
+            L.seq = ip ? (uint32_t)__popcll(ipm & lt) : (uint32_t)(__popcll(ipm) + __popcll(rndm & lt));
+        }
+        ctr = (uint32_t)__popcll(ipm | rndm);
+        return 0;
+    };
+
+    auto place = [&]() -> bool {
+        const int r = position_reset_jacobi();
+        if (r == 2) return position_reset_lanes();
+        return r == 0;
+    };
 #ifdef GW_STAMPS
     const int e = blockIdx.x;
 #endif

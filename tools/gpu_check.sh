@@ -1,13 +1,21 @@
 #!/bin/bash
-# GPU round: tests, bench, stamps (each step time-limited; stop at first failure)
+# GPU round: [checks-build tests], tests, bench, [stamps]; each step
+# time-limited, stop at the first failure.
+#   tools/gpu_check.sh [checks] [stamps]
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+ARGS=" $* "
+if [[ "$ARGS" == *" checks "* ]]; then
+  GW_ENGINE_VARIANT=checks timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests_checks.log 2>&1
+  rc=$?; tail -3 gpurun_out/gpu_tests_checks.log
+  [ $rc -eq 0 ] || { echo "CHECKS TESTS FAILED rc=$rc"; tail -60 gpurun_out/gpu_tests_checks.log; exit 1; }
+fi
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
-rc=$?; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || { echo "TESTS FAILED rc=$rc"; tail -60 gpurun_out/gpu_tests.log; exit 1; }
+rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || { echo "TESTS FAILED rc=$rc"; tail -60 gpurun_out/gpu_tests.log; exit 1; }
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH FAIL; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-if [ "$1" == "stamps" ]; then
+if [[ "$ARGS" == *" stamps "* ]]; then
   timeout -k 10 300 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { echo STAMPS FAIL; tail -20 gpurun_out/stamps.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/stamps.log
 fi
