@@ -352,9 +352,17 @@ struct Smem {
     int8_t* stage;
 };
 
-// Jacobi placement scratch (do_reset): words [JAC_WB] u32 | pub [64] uint2 | key2 [624] u32
+// Jacobi placement scratch in the work area (do_reset): stream words,
+// per-lane (fresh, enc), chunk prefix counts, lane bits by cell rank, their
+// prefix ORs, and a twisted copy of the key
 constexpr int JAC_WB = 192;
-constexpr size_t JAC_WORK_BYTES = 4 * JAC_WB + 8 * 64 + 4 * GW_MT_N;
+constexpr int JAC_OFF_W = 0;
+constexpr int JAC_OFF_PUB = JAC_OFF_W + 4 * JAC_WB;
+constexpr int JAC_OFF_CP = JAC_OFF_PUB + 8 * 64;
+constexpr int JAC_OFF_SB = JAC_OFF_CP + 4 * 64;
+constexpr int JAC_OFF_T = JAC_OFF_SB + 8 * 64;
+constexpr int JAC_OFF_KEY2 = JAC_OFF_T + 8 * 64;
+constexpr size_t JAC_WORK_BYTES = JAC_OFF_KEY2 + 4 * GW_MT_N;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -853,26 +861,41 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     // the cell, which lists the cell was freshly removed from) is re-derived
     // each sweep from the other lanes' current estimates, until a sweep
     // changes nothing.  Lane i only depends on lanes placed before it, so the
-    // fixed point is the sequential result; the cell is checked to be the
-    // LEAST fixpoint of c = idx + #{removed <= c} (a larger one sits on a
-    // removed cell).  Returns 0 placed, 1 placement exception (err set),
-    // 2 unresolved (more than JAC_WB words / sweep cap): run the serial loop.
+    // fixed point is the sequential result.  Per sweep the estimates are
+    // ranked by cell (histogram in the count table + chunk prefix sums), and
+    // T[r] = the lanes holding the r+1 lowest cells, so "removed cells <= c"
+    // is popc(T[rank(c)-1] & removers-before-me): the least fixpoint of
+    // c = idx + #{removed <= c} costs a few LDS reads (a fixpoint on a
+    // removed cell is not the least: restart from idx).  Returns 0 placed,
+    // 1 placement exception (err set), 2 unresolved (word buffer / sweep
+    // cap / a full list): run the serial loop.
     auto position_reset_jacobi = [&]() -> int {
         constexpr int MAX_SWEEPS = 48;
+#ifdef GW_STAMPS
+        uint64_t acc_t[5] = {0, 0, 0, 0, 0};
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+        int nsw = 0;
+#endif
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         const bool ip = valid && L.init_r >= 0;
         const bool rnd = valid && !ip;
         const uint64_t ipm = __ballot(ip), rndm = __ballot(rnd);
         const int nrnd = __popcll(rndm);
         if (nrnd + 8 > JAC_WB) return 2;
-        const uint64_t lt = (1ull << l) - 1ull;
-        const uint32_t ord = valid ? (ip ? (uint32_t)l : 64u + (uint32_t)l) : 255u;
-        const uint64_t before = ip ? (ipm & lt) : (ipm | (rndm & lt));
+        const uint64_t lt_l = (1ull << l) - 1ull;
+        const uint64_t before = ip ? (ipm & lt_l) : (rnd ? (ipm | (rndm & lt_l)) : 0ull);
         const uint32_t rem = valid ? (p.no_overlap_at_reset ? all_encs : (all_encs & ~L.ov)) : 0u;
-        const uint32_t encbit = 1u << L.enc;
-        uint32_t* wbuf = (uint32_t*)sm.stage;
-        uint2* pub = (uint2*)(sm.stage + 4 * JAC_WB);
-        uint32_t* key2 = (uint32_t*)(sm.stage + 4 * JAC_WB + 8 * 64);
+        uint32_t* wbuf = (uint32_t*)(sm.stage + JAC_OFF_W);
+        uint2* pub = (uint2*)(sm.stage + JAC_OFF_PUB);
+        uint32_t* cpa = (uint32_t*)(sm.stage + JAC_OFF_CP);
+        uint2* sb = (uint2*)(sm.stage + JAC_OFF_SB);
+        uint2* tb = (uint2*)(sm.stage + JAC_OFF_T);
+        uint32_t* key2 = (uint32_t*)(sm.stage + JAC_OFF_KEY2);
+        uint32_t* hist = sm.cnt;   // rebuilt by build_tables afterwards
+        const int nw = (HW + 3) >> 2;
+        int chs = 2;               // chunk of 1 << chs cells per lane
+        while ((WAVE << chs) < HW) chs++;
+        const int cw = 1 << (chs - 2);
         const int pos0 = rng.pos;
         const bool crosses = pos0 + JAC_WB > GW_MT_N;
         wave_sync();
@@ -893,21 +916,41 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             }
             wave_sync();
         }
-        int cell = ip ? L.init_r * p.W + L.init_c : HW + l;   // distinct off-grid guesses
+        ACC_T(0, t0);
+        // #cells <= c among this sweep's estimates (lt: < c)
+        auto rank_le = [&](int c, uint32_t& lt) -> uint32_t {
+            const int k = c >> chs;
+            uint32_t sum = cpa[CIDX(k, WAVE, 14)];
+            const int wc = c >> 2;
+            for (int w = k * cw; w < wc; w++) sum = __builtin_amdgcn_sad_u8(hist[w], 0u, sum);
+            const uint32_t hw = hist[CIDX(wc, nw, 15)];
+            const int sh = 8 * (c & 3);
+            sum = __builtin_amdgcn_sad_u8(hw & ((1u << sh) - 1u), 0u, sum);
+            lt = sum;
+            return sum + ((hw >> sh) & 0xffu);
+        };
+        auto lanes_upto = [&](uint32_t r) -> uint64_t {   // lanes of the r lowest cells
+            if (r == 0) return 0ull;
+            const uint2 t = tb[CIDX((int)r - 1, WAVE, 16)];
+            return ((uint64_t)t.y << 32) | t.x;
+        };
+        int cell = ip ? L.init_r * p.W + L.init_c : 0;
         uint32_t fresh = rem;
         int used = rnd ? 1 : 0;
-        int idx = -1;
+        int idx = rnd ? -1 : 0;
         uint32_t n = 0;
         bool bad = false, qbad = false;
         for (int sweep = 0;; sweep++) {
             if (sweep == MAX_SWEEPS) return 2;
-            // |list enc| when this lane is placed
+            // |list enc| when this lane is placed, and who shortened it
             uint64_t mym = 0;
             for (int f = 1; f <= p.max_enc; f++) {
                 const uint64_t m = __ballot((fresh >> f) & 1u);
                 if (L.enc == f) mym = m;
             }
-            n = (uint32_t)HW - (uint32_t)__popcll(mym & before);
+            const uint64_t rm = mym & before;
+            n = (uint32_t)HW - (uint32_t)__popcll(rm);
+            ACC_T(1, t0);
             // interval(n - 1) draws: stream offsets = exclusive scan of words
             // used; iterate until consistent (each pass fixes the first lane)
             const bool draws = rnd && n > 1;
@@ -934,36 +977,77 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 used = nu;
                 if (!ch) break;
             }
-            // cells: count removed cells <= the current estimate
-            if (valid) pub[l] = make_uint2((uint32_t)cell | (ord << 16) | ((uint32_t)L.enc << 24), fresh);
+            ACC_T(2, t0);
+            // rank this sweep's cell estimates
+            const int ce0 = rnd ? (nidx != idx ? nidx : cell) : cell;
+            for (int i = l; i < nw; i += WAVE) hist[i] = 0u;
+            if (valid) pub[l] = make_uint2(fresh, (uint32_t)L.enc);
+            sb[l] = make_uint2(0u, 0u);
             wave_sync();
-            const int ce = (nidx != idx) ? nidx : cell;
-            int cnt = 0;
-            bool inR = false, qb = false;
-            uint32_t dup = 0;
-#pragma unroll 4
-            for (int j = 0; j < A; j++) {
-                const uint2 q = pub[j];
-                const int cj = (int)(q.x & 0xffffu);
-                const bool bef = ((q.x >> 16) & 0xffu) < ord;
-                const bool rj = bef && (q.y & encbit);
-                cnt += (rj && cj <= ce) ? 1 : 0;
-                inR |= rj && cj == ce;
-                if (bef && cj == cell) {
-                    dup |= q.y;
-                    qb |= !((L.ov >> (q.x >> 24)) & 1u);
+            uint32_t tie = 0;
+            if (valid) {
+                const int sh = 8 * (ce0 & 3);
+                tie = (atomicAdd(&hist[CIDX(ce0 >> 2, nw, 17)], 1u << sh) >> sh) & 0xffu;
+            }
+            wave_sync();
+            uint32_t csum = 0;
+            for (int w = 0; w < cw; w++) {
+                const int wi = l * cw + w;
+                if (wi < nw) csum = __builtin_amdgcn_sad_u8(hist[wi], 0u, csum);
+            }
+            cpa[l] = wave_incl_scan(csum) - csum;
+            wave_sync();
+            if (valid) {
+                uint32_t lt0;
+                rank_le(ce0, lt0);
+                sb[CIDX((int)(lt0 + tie), WAVE, 18)] = l < 32 ? make_uint2(1u << l, 0u) : make_uint2(0u, 1u << (l - 32));
+            }
+            wave_sync();
+            {
+                const uint2 sv = sb[l];
+                tb[l] = make_uint2(wave_incl_scan(sv.x), wave_incl_scan(sv.y));
+            }
+            wave_sync();
+            // least fixpoint of c = idx + #{removed cells <= c}
+            int c = ce0;
+            bool fin = !rnd, ovf = false;
+            uint64_t eqm = 0;
+            for (int it = 0;; it++) {
+                uint32_t lt;
+                const uint32_t le = rank_le(c, lt);
+                const uint64_t mle = lanes_upto(le);
+                eqm = mle & ~lanes_upto(lt);
+                if (!fin) {
+                    const int c2 = nidx + __popcll(mle & rm);
+                    if (c2 >= HW) { ovf = true; fin = true; }
+                    else if (c2 != c) c = c2;
+                    else if (eqm & rm) c = nidx;   // on a removed cell: not the least
+                    else fin = true;
                 }
+                if (__ballot(!fin) == 0) break;
+                if (it == 2 * WAVE) { ovf = ovf || !fin; break; }
+            }
+            // earlier placements on the same cell: lists already shortened
+            // by it, and Grid.query for initial positions
+            uint64_t dm = valid ? (eqm & before) : 0ull;
+            uint32_t dup = 0;
+            bool qb = false;
+            while (dm) {
+                const int j = __builtin_ctzll(dm);
+                dm &= dm - 1ull;
+                const uint2 pj = pub[j];
+                dup |= pj.x;
+                qb |= !((L.ov >> pj.y) & 1u);
             }
             wave_sync();
-            int cn = cell;
-            if (rnd) {
-                cn = nidx + cnt;
-                if (inR && cn == ce) cn = nidx;   // a fixpoint on a removed cell is not the least
-            }
             const uint32_t nf = rem & ~dup;
-            const bool lane_ch = valid && (cn != cell || nf != fresh || nidx != idx || (rnd && inR));
+            const bool lane_ch = valid && (ovf || c != ce0 || nf != fresh || nidx != idx);
             const bool any = __ballot(lane_ch) != 0;
-            cell = cn; fresh = nf; idx = nidx; qbad = qb;
+            cell = c; fresh = nf; idx = nidx; qbad = qb;
+            ACC_T(3, t0);
+#ifdef GW_STAMPS
+            nsw++;
+#endif
             if (!any) break;
         }
         if (__ballot(bad)) return 2;
@@ -984,9 +1068,16 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         if (valid) {
             L.in_grid = true;
             L.r = cell / p.W; L.c = cell % p.W;
-            L.seq = ip ? (uint32_t)__popcll(ipm & lt) : (uint32_t)(__popcll(ipm) + __popcll(rndm & lt));
+            L.seq = ip ? (uint32_t)__popcll(ipm & lt_l) : (uint32_t)(__popcll(ipm) + __popcll(rndm & lt_l));
         }
         ctr = (uint32_t)__popcll(ipm | rndm);
+        ACC_T(4, t0);
+#ifdef GW_STAMPS
+        if (l == 0 && p.stamps) {
+            for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * 32 + 20 + k] = acc_t[k];
+            p.stamps[(size_t)blockIdx.x * 32 + 25] = nsw;
+        }
+#endif
         return 0;
     };
 

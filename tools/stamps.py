@@ -64,7 +64,8 @@ def main():
                 resets.append(np.stack([rs[:, 10] - rs[:, 0], rs[:, 13] - rs[:, 12],
                                         rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0],
                                         rs[:, 11] - rs[:, 12], rs[:, 15] - rs[:, 11],
-                                        rs[:, 16], rs[:, 17], rs[:, 18], rs[:, 19]], 1))
+                                        rs[:, 16], rs[:, 17], rs[:, 18], rs[:, 19],
+                                        rs[:, 20], rs[:, 21], rs[:, 22], rs[:, 23], rs[:, 24], rs[:, 25]], 1))
     d = np.concatenate(deltas)
     tot = d.sum(1)
     print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
@@ -87,6 +88,9 @@ def main():
               f"health {np.median(r[:, 5]):.0f}")
         print(f"placement loop parts (median sums): head {np.median(r[:, 6]):.0f} draw "
               f"{np.median(r[:, 7]):.0f} fixpoint {np.median(r[:, 8]):.0f} update {np.median(r[:, 9]):.0f}")
+        print(f"jacobi (median sums): words {np.median(r[:, 10]):.0f} lens {np.median(r[:, 11]):.0f} "
+              f"draws {np.median(r[:, 12]):.0f} cells {np.median(r[:, 13]):.0f} commit "
+              f"{np.median(r[:, 14]):.0f}; sweeps median {np.median(r[:, 15]):.0f} max {r[:, 15].max()}")
 
 
 if __name__ == '__main__':
