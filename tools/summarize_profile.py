@@ -20,6 +20,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def short_name(n):
+    """'void (anonymous namespace)::step_kernel<7>((anonymous namespace)::Params)'
+    -> 'step_kernel<7>'"""
+    n = n.replace('(anonymous namespace)::', '')
+    if n.startswith('void '):
+        n = n[5:]
+    return n.split('(')[0][:60]
+
+
 def main():
     tag = sys.argv[1]
     kname = sys.argv[2] if len(sys.argv) > 2 else 'step_kernel'
@@ -32,8 +41,8 @@ def main():
     trace = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_trace.csv'))))
     res = {}
     for r in trace:
-        if kname in r['Kernel_Name']:
-            res = {k: r[k] for k in ('LDS_Block_Size', 'Scratch_Size', 'VGPR_Count',
+        if kname in short_name(r['Kernel_Name']):
+            res = {k: r.get(k, '') for k in ('LDS_Block_Size', 'Scratch_Size', 'VGPR_Count',
                                      'Accum_VGPR_Count', 'SGPR_Count', 'Workgroup_Size_X',
                                      'Grid_Size_X')}
             break
@@ -55,8 +64,7 @@ def main():
              "`--pmc WRITE_SIZE`, separate runs, `--steps 30 --warmup 5`).", "",
              "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
     for r in rows[:8]:
-        n = r['Name']
-        n = n.split('(')[0] if 'anonymous' in n else n[:60]
+        n = short_name(r['Name'])
         lines.append(f"| `{n}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
                      f"{float(r['MinNs'])/1e3:.2f} | {float(r['MaxNs'])/1e3:.2f} | "
                      f"{float(r['Percentage']):.1f} |")
@@ -70,7 +78,7 @@ def main():
         lines += [f"PMC per {kname} launch: FETCH_SIZE {fetch_b/1e6:.2f} MB, WRITE_SIZE "
                   f"{write_b/1e6:.2f} MB, sum {(fetch_b+write_b)/1e6:.2f} MB (raw, uncorrected)."]
     for r in rows:
-        if kname in r['Name']:
+        if kname in short_name(r['Name']):
             out['avg_ns'] = float(r['AverageNs'])
     json.dump(out, open(os.path.join(dst, f'pmc_{kname}.json'), 'w'), indent=1)
     open(os.path.join(dst, f'{tag}_summary.md'), 'w').write('\n'.join(lines) + '\n')
