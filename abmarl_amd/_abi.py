@@ -6,6 +6,7 @@ integers (``tensor.data_ptr()``) and streams as ``void*``.
 import ctypes as C
 
 GW_MAX_AGENTS = 64
+GW_MAX_ENTITIES = 4096
 GW_MAX_ENC = 15
 GW_MAX_CELLS = 4096
 GW_MAX_RANGE = 7

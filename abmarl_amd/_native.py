@@ -40,6 +40,8 @@ SIGNATURES = {
     'gw_destroy': (_i32, [_vp]),
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),
+    'gw_num_lanes': (_i32, [_vp]),
+    'gw_lane_entities': (_i32, [_vp, _vp]),
     'gw_last_error': (C.c_char_p, []),
     'gw_abi_version': (_i32, []),
 }

@@ -41,6 +41,8 @@
 #include <string.h>
 #include <stdarg.h>
 #include <stdlib.h>
+#include <vector>
+#include <type_traits>
 
 #include "../../include/gw_engine.h"
 
@@ -83,7 +85,30 @@ struct Params {
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
+    // static entities (gw_engine.h "Entities and lanes") and blocking
+    int32_t n_free;                        // cells not held by a static entity
+    const uint16_t* free_cell;             // [n_free] free index -> cell; NULL = identity
+    const uint16_t* cell_free;             // [HW] cell -> free index
+    const uint32_t* static_bits;           // [ceil(HW/32)] static cells; NULL = none
+    uint32_t static_encs;                  // encodings of static entities (always active)
+    int32_t blockers;                      // any blocking entity
+    int32_t lane_blockers;                 // any blocking lane
+    // shadow LUT: range r, blocker at (dr, dc): mask_words(r) words at
+    // shadow_off[r] + ((dr+r)(2r+1) + dc+r) * mask_words(r); bit k = window
+    // cell k (row-major) hidden (utils.py:46-115)
+    const uint32_t* shadow;
+    // hidden cells due to static blockers for an entity at `cell`, range r:
+    // smask_off[r] + cell * mask_words(r) (smask_off[r] < 0: not built)
+    const uint32_t* smask;
+    int32_t shadow_off[GW_MAX_RANGE + 1];
+    int32_t smask_off[GW_MAX_RANGE + 1];
 };
+
+__host__ __device__ inline int mask_words(int r)
+{
+    const int d = 2 * r + 1;
+    return (d * d + 31) >> 5;
+}
 
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ void wave_sync()
@@ -490,41 +515,78 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
     bool has_ev = false;
 
-    if (l < A) {
-        int8_t* st = sm.stage + l * SS;
-        if (obs_me) {
-            const uint32_t* t32 = (const uint32_t*)sm.tbl;
-            uint32_t rows[S][ND];
-            // every window row's dwords first (independent LDS reads), then decode
-            const int o0 = tbl_idx(p, L.r - R, L.c - R);
+    // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
+    // static blockers precomputed per cell, blocking lanes from the shadow LUT
+    constexpr int MW = (SS + 31) / 32;
+    uint32_t hid[MW];
 #pragma unroll
-            for (int wr = 0; wr < S; wr++) {
-                const int o = o0 + wr * p.pitch;
+    for (int w = 0; w < MW; w++) hid[w] = 0u;
+    if (p.blockers) {
+        if (obs_me && p.smask_off[R] >= 0) {
+            const uint32_t* src = p.smask + p.smask_off[R] + (size_t)(L.r * p.W + L.c) * MW;
 #pragma unroll
-                for (int d = 0; d < ND; d++)
-                    rows[wr][d] = t32[CIDX((o >> 2) + d, (p.tbl_rows * p.pitch + 3) / 4, 2)];
+            for (int w = 0; w < MW; w++) hid[w] = src[w];
+        }
+        if (p.lane_blockers) {
+            for (uint64_t bl = __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
+                const int b = first_lane(bl);
+                const int dr = rl(L.r, b) - L.r, dc = rl(L.c, b) - L.c;
+                if (obs_me && dr >= -R && dr <= R && dc >= -R && dc <= R && (dr != 0 || dc != 0)) {
+                    const uint32_t* src = p.shadow + p.shadow_off[R] + ((dr + R) * S + (dc + R)) * MW;
+#pragma unroll
+                    for (int w = 0; w < MW; w++) hid[w] |= src[w];
+                }
             }
-            const int sh = o0 & 3;
+        }
+    }
+
+    // window rows -> int8 stage: every row's dwords first (independent LDS
+    // reads), then decode; hidden cells are -2 and never draw
+    auto stage_rows = [&](auto masked) {
+        constexpr bool MASKED = decltype(masked)::value;
+        int8_t* st = sm.stage + l * SS;
+        const uint32_t* t32 = (const uint32_t*)sm.tbl;
+        uint32_t rows[S][ND];
+        const int o0 = tbl_idx(p, L.r - R, L.c - R);
 #pragma unroll
-            for (int wr = 0; wr < S; wr++) {
+        for (int wr = 0; wr < S; wr++) {
+            const int o = o0 + wr * p.pitch;
 #pragma unroll
-                for (int d = 0; d + 1 < ND; d++) {
-                    const uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
-                    const uint32_t ev = w & 0x80808080u & ~(w << 1);
+            for (int d = 0; d < ND; d++)
+                rows[wr][d] = t32[CIDX((o >> 2) + d, (p.tbl_rows * p.pitch + 3) / 4, 2)];
+        }
+        const int sh = o0 & 3;
 #pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        const int wc = d * 4 + b;
-                        if (wc < S) {
-                            uint32_t v = (w >> (8 * b)) & 0xffu;
-                            if (wr == R && wc == R && !p.observe_self && L.in_grid && v != CELL_CROWD)
-                                v = 0;                      // alone on my cell, not observing myself
-                            st[wr * S + wc] = (int8_t)v;
-                            has_ev |= ((ev >> (8 * b)) & 0x80u) != 0;
+        for (int wr = 0; wr < S; wr++) {
+#pragma unroll
+            for (int d = 0; d + 1 < ND; d++) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
+                const uint32_t ev = w & 0x80808080u & ~(w << 1);
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int wc = d * 4 + b;
+                    if (wc < S) {
+                        uint32_t v = (w >> (8 * b)) & 0xffu;
+                        if (wr == R && wc == R && !p.observe_self && L.in_grid && v != CELL_CROWD)
+                            v = 0;                      // alone on my cell, not observing myself
+                        bool crowd = ((ev >> (8 * b)) & 0x80u) != 0;
+                        if constexpr (MASKED) {
+                            const int kk = wr * S + wc;
+                            if ((hid[kk >> 5] >> (kk & 31)) & 1u) { v = 0xFEu; crowd = false; }
                         }
+                        st[wr * S + wc] = (int8_t)v;
+                        has_ev |= crowd;
                     }
                 }
             }
+        }
+    };
+    if (l < A) {
+        if (obs_me) {
+            if (p.blockers) stage_rows(std::integral_constant<bool, true>());
+            else stage_rows(std::integral_constant<bool, false>());
         } else {
+            int8_t* st = sm.stage + l * SS;
             for (int k = 0; k < SS; k++) st[k] = -2;
         }
     }
@@ -618,8 +680,26 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     const uint32_t amap = rl(L.amap, a);
     const int D = 2 * R + 1;
     const int dr = L.r - ar, dc = L.c - ac;
-    const bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
-                      dr >= -R && dr <= R && dc >= -R && dc <= R;
+    bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
+                dr >= -R && dr <= R && dc >= -R && dc <= R;
+    if (p.blockers) {                                       // attack mask (actor.py:483-494)
+        const int k = (dr + R) * D + (dc + R), mw = mask_words(R);
+        bool hidden = false;
+        if (cand && p.smask_off[R] >= 0)
+            hidden = (p.smask[p.smask_off[R] + (size_t)(ar * p.W + ac) * mw + (k >> 5)] >> (k & 31)) & 1u;
+        if (p.lane_blockers) {
+            for (uint64_t bl = __ballot(l < p.A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
+                const int b = first_lane(bl);
+                const int bdr = rl(L.r, b) - ar, bdc = rl(L.c, b) - ac;
+                if (bdr < -R || bdr > R || bdc < -R || bdc > R || (bdr == 0 && bdc == 0)) continue;
+                if (cand) {
+                    const uint32_t* src = p.shadow + p.shadow_off[R] + ((bdr + R) * D + (bdc + R)) * mw;
+                    hidden = hidden || ((src[k >> 5] >> (k & 31)) & 1u);
+                }
+            }
+        }
+        cand = cand && !hidden;
+    }
     const uint32_t ckey = ((uint32_t)((dr + R) * D + (dc + R)) << 24) | L.seq;
     const uint64_t cm = __ballot(cand);
     // rank of every candidate in (window cell, insertion) order
@@ -703,6 +783,10 @@ __device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr
     const int nr = ar + mr, nc = ac + mc;
     if (!(0 <= nr && nr < p.H && 0 <= nc && nc < p.W)) return false;
     if (nr == ar && nc == ac) return true;
+    if (p.static_bits) {                                    // a static entity: overlaps nothing
+        const int cell = nr * p.W + nc;
+        if ((p.static_bits[cell >> 5] >> (cell & 31)) & 1u) return false;
+    }
     const uint32_t aov = rl(L.ov, a);
     const bool blocks = l < p.A && L.in_grid && L.r == nr && L.c == nc && !((aov >> L.enc) & 1u);
     if (__ballot(blocks)) return false;                     // Grid.query
@@ -733,7 +817,11 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
-    const int HW = p.H * p.W;
+    // placement works in free-cell space: the cells no static entity holds
+    // (every list lost them before the first draw); NF = p.n_free
+    const int NF = p.n_free;
+    auto to_cell = [&](int f) -> int { return p.free_cell ? (int)p.free_cell[CIDX(f, NF, 19)] : f; };
+    auto to_free = [&](int cell) -> int { return p.cell_free ? (int)p.cell_free[CIDX(cell, p.H * p.W, 19)] : cell; };
     L.live = valid && (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
     L.in_grid = false;
     L.reward = 0.0;
@@ -796,7 +884,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     auto position_reset_lanes = [&]() -> bool {
         int cell_l = -1;                 // this lane's cell once placed
         uint32_t remeff = 0;             // lists this lane's placement shortened
-        uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)HW : 0u;
+        uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)NF : 0u;
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         for (int pass = 0; pass < 2; pass++) {
             for (int a = 0; a < A; a++) {
@@ -812,7 +900,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 ACC_T(0, t0);
                 if (has_ip) {
                     const int ic = rl(L.init_c, a);
-                    cell = ir * p.W + ic;
+                    cell = to_free(ir * p.W + ic);
                     // Grid.place -> query (grid.py:81-129), asserted by the reference
                     const bool blocks = valid && L.in_grid && cell_l == cell && !((aov >> L.enc) & 1u);
                     if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
@@ -829,7 +917,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                         c = c2;
                     }
                     cell = uni(c);
-                    CHECK(cell >= 0 && cell < HW, 7, cell, a);
+                    CHECK(cell >= 0 && cell < NF, 7, cell, a);
                     // a cell taken from list aenc always passes Grid.query
                     ACC_T(2, t0);
                 }
@@ -848,7 +936,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 ACC_T(3, t0);
             }
         }
-        if (L.in_grid) { L.r = cell_l / p.W; L.c = cell_l % p.W; }
+        if (L.in_grid) { const int gc = to_cell(cell_l); L.r = gc / p.W; L.c = gc % p.W; }
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps)
             for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * 32 + 16 + k] = acc_t[k];
@@ -892,9 +980,9 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint2* tb = (uint2*)(sm.stage + JAC_OFF_T);
         uint32_t* key2 = (uint32_t*)(sm.stage + JAC_OFF_KEY2);
         uint32_t* hist = sm.cnt;   // rebuilt by build_tables afterwards
-        const int nw = (HW + 3) >> 2;
+        const int nw = (NF + 3) >> 2;
         int chs = 2;               // chunk of 1 << chs cells per lane
-        while ((WAVE << chs) < HW) chs++;
+        while ((WAVE << chs) < NF) chs++;
         const int cw = 1 << (chs - 2);
         const int pos0 = rng.pos;
         const bool crosses = pos0 + JAC_WB > GW_MT_N;
@@ -934,7 +1022,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             const uint2 t = tb[CIDX((int)r - 1, WAVE, 16)];
             return ((uint64_t)t.y << 32) | t.x;
         };
-        int cell = ip ? L.init_r * p.W + L.init_c : 0;
+        int cell = ip ? to_free(L.init_r * p.W + L.init_c) : 0;
         uint32_t fresh = rem;
         int used = rnd ? 1 : 0;
         int idx = rnd ? -1 : 0;
@@ -949,7 +1037,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 if (L.enc == f) mym = m;
             }
             const uint64_t rm = mym & before;
-            n = (uint32_t)HW - (uint32_t)__popcll(rm);
+            n = (uint32_t)NF - (uint32_t)__popcll(rm);
             ACC_T(1, t0);
             // interval(n - 1) draws: stream offsets = exclusive scan of words
             // used; iterate until consistent (each pass fixes the first lane)
@@ -1019,7 +1107,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 eqm = mle & ~lanes_upto(lt);
                 if (!fin) {
                     const int c2 = nidx + __popcll(mle & rm);
-                    if (c2 >= HW) { ovf = true; fin = true; }
+                    if (c2 >= NF) { ovf = true; fin = true; }
                     else if (c2 != c) c = c2;
                     else if (eqm & rm) c = nidx;   // on a removed cell: not the least
                     else fin = true;
@@ -1064,10 +1152,11 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             rng.pos = np;
         }
         rng.base = -1;
-        CHECK(!valid || (cell >= 0 && cell < HW), 7, cell, l);
+        CHECK(!valid || (cell >= 0 && cell < NF), 7, cell, l);
         if (valid) {
             L.in_grid = true;
-            L.r = cell / p.W; L.c = cell % p.W;
+            const int gc = to_cell(cell);
+            L.r = gc / p.W; L.c = gc % p.W;
             L.seq = ip ? (uint32_t)__popcll(ipm & lt_l) : (uint32_t)(__popcll(ipm) + __popcll(rndm & lt_l));
         }
         ctr = (uint32_t)__popcll(ipm | rndm);
@@ -1279,9 +1368,10 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         all = dn;
     } else {
         all = true;
-        if (p.done_kind & GW_DONE_ACTIVE) all = all && (__ballot(valid && L.active) == 0);
+        // static entities are agents too, always active (done.py:49-56,147-153)
+        if (p.done_kind & GW_DONE_ACTIVE) all = all && p.static_encs == 0 && (__ballot(valid && L.active) == 0);
         if (p.done_kind & GW_DONE_ONE_TEAM) {
-            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u);
+            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u) | p.static_encs;
             all = all && (__popc(bits) <= 1);
         }
     }
@@ -1387,8 +1477,52 @@ struct gw_engine {
     Params base;
     DevAgent* d_spec;
     uint4* d_tmpl;
+    uint16_t* d_free;          // free_cell | cell_free
+    uint32_t* d_static_bits;
+    uint32_t* d_shadow;
+    uint32_t* d_smask;
+    int32_t lane_ent[GW_MAX_AGENTS];
     size_t smem_step, smem_reset;
 };
+
+// create_grid_and_mask (utils.py:46-115): the window cells of range R that a
+// blocker at offset (rd, cd) hides, as bits k = (r+R)(2R+1) + (c+R).  The
+// eight cases differ only in the half-plane scanned and in the +-0.5
+// offsets of the two rays; the arithmetic is the reference's, in double.
+static void host_shadow(int R, int rd, int cd, uint32_t* bits)
+{
+    const int D = 2 * R + 1;
+    for (int w = 0; w < mask_words(R); w++) bits[w] = 0u;
+    if (rd == 0 && cd == 0) return;
+    const double r_d = rd, c_d = cd;
+    for (int r = -R; r <= R; r++) {
+        for (int c = -R; c <= R; c++) {
+            if (r == rd && c == cd) continue;                      // not the blocker itself
+            bool hide = false;
+            if (cd == 0) {                                          // below / above: rays in c
+                if (rd > 0 ? r < rd : r > rd) continue;
+                const double dd = rd > 0 ? -0.5 : 0.5;
+                const double left = (c_d - 0.5) / (r_d + dd) * r, right = (c_d + 0.5) / (r_d + dd) * r;
+                hide = left < c && c < right;
+            } else {                                                // rays in r
+                if (cd > 0 ? c < cd : c > cd) continue;
+                if (rd > 0 && r < rd) continue;
+                if (rd < 0 && r > rd) continue;
+                // offsets of (rd -+ 0.5) / (cd + lo_d | up_d) per case
+                double lo_d, up_d;
+                if (rd == 0) { lo_d = up_d = cd > 0 ? -0.5 : 0.5; }             // right / left
+                else if ((rd > 0) == (cd > 0)) { lo_d = 0.5; up_d = -0.5; }     // below-right / above-left
+                else { lo_d = -0.5; up_d = 0.5; }                               // below-left / above-right
+                const double lo = (r_d - 0.5) / (c_d + lo_d) * c, up = (r_d + 0.5) / (c_d + up_d) * c;
+                hide = lo < r && r < up;
+            }
+            if (hide) {
+                const int k = (r + R) * D + (c + R);
+                bits[k >> 5] |= 1u << (k & 31);
+            }
+        }
+    }
+}
 
 static thread_local char g_err[512];
 
@@ -1463,15 +1597,15 @@ static hipError_t set_attrs(int S, size_t a, size_t b)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 1; }
+int32_t gw_abi_version(void) { return 2; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
 {
     if (!cfg || !out || n_envs <= 0) { set_err("invalid argument"); return GW_E_INVALID; }
-    const int A = cfg->n_agents, HW = cfg->rows * cfg->cols;
-    if (A <= 0 || A > GW_MAX_AGENTS) {
-        set_err("n_agents=%d outside 1..%d (one wavefront lane per entity)", A, GW_MAX_AGENTS);
+    const int NE = cfg->n_agents, HW = cfg->rows * cfg->cols;
+    if (NE <= 0 || NE > GW_MAX_ENTITIES) {
+        set_err("n_agents=%d outside 1..%d", NE, GW_MAX_ENTITIES);
         return GW_E_UNSUPPORTED;
     }
     if (cfg->rows <= 0 || cfg->cols <= 0 || HW > GW_MAX_CELLS) {
@@ -1487,29 +1621,70 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         return GW_E_INVALID;
     }
     int max_enc = 0;
-    for (int a = 0; a < A; a++) {
+    for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
         if (s.encoding < 1 || s.encoding > GW_MAX_ENC) { set_err("agent %d encoding %d", a, s.encoding); return GW_E_UNSUPPORTED; }
-        if (s.kind & GW_K_BLOCKING) { set_err("blocking agents are not built yet"); return GW_E_UNSUPPORTED; }
         if ((s.kind & GW_K_GRID_OBSERVER) && s.view_range != cfg->obs_range) {
             set_err("agent %d view_range %d != obs_range %d", a, s.view_range, cfg->obs_range);
             return GW_E_UNSUPPORTED;
         }
-        if ((s.kind & GW_K_ATTACKING) && s.attack_range > GW_MAX_RANGE) { set_err("attack_range"); return GW_E_UNSUPPORTED; }
+        if ((s.kind & GW_K_ATTACKING) && (s.attack_range < 0 || s.attack_range > GW_MAX_RANGE)) {
+            set_err("agent %d attack_range %d", a, s.attack_range);
+            return GW_E_UNSUPPORTED;
+        }
         if (s.init_row >= cfg->rows || s.init_col >= cfg->cols) { set_err("agent %d initial position outside the grid", a); return GW_E_INVALID; }
         if (s.encoding > max_enc) max_enc = s.encoding;
     }
-    if (cfg->sim_kind == GW_SIM_MAZE_NAV &&
-        (cfg->nav_agent < 0 || cfg->nav_agent >= A || cfg->target_agent < 0 || cfg->target_agent >= A)) {
+    const bool maze = cfg->sim_kind == GW_SIM_MAZE_NAV;
+    if (maze && (cfg->nav_agent < 0 || cfg->nav_agent >= NE || cfg->target_agent < 0 || cfg->target_agent >= NE)) {
         set_err("maze navigation needs nav_agent/target_agent");
         return GW_E_INVALID;
     }
+    // ---- entities -> static entities | lanes (gw_engine.h "Entities and lanes")
+    uint32_t attacked = 0, overlapped = 0;
+    for (int e = 0; e <= GW_MAX_ENC; e++) { attacked |= cfg->attack_mapping[e]; overlapped |= cfg->overlap[e]; }
+    const uint32_t dynamic_kinds = GW_K_OBSERVING | GW_K_ACTING | GW_K_GRID_OBSERVER | GW_K_MOVING |
+                                   GW_K_ATTACKING | GW_K_HEALTH;
+    std::vector<int> lanes, statics;
+    for (int a = 0; a < NE; a++) {
+        const gw_agent_spec& s = cfg->agents[a];
+        const bool st = !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
+                        cfg->overlap[s.encoding] == 0 && !((overlapped >> s.encoding) & 1u) &&
+                        !((attacked >> s.encoding) & 1u) &&
+                        !(maze && (a == cfg->nav_agent || a == cfg->target_agent));
+        (st ? statics : lanes).push_back(a);
+    }
+    const int A = (int)lanes.size();
+    if (A == 0 || A > GW_MAX_AGENTS) {
+        set_err("%d dynamic entities outside 1..%d (one wavefront lane each)", A, GW_MAX_AGENTS);
+        return GW_E_UNSUPPORTED;
+    }
+    std::vector<uint8_t> is_static(HW, 0);
+    for (int a : statics) {
+        const int cell = cfg->agents[a].init_row * cfg->cols + cfg->agents[a].init_col;
+        if (is_static[cell]) {   // Grid.place of the second one fails at every reset
+            set_err("static entities %d share cell %d (the reference raises at every reset)", a, cell);
+            return GW_E_INVALID;
+        }
+        is_static[cell] = 1;
+    }
+    for (int a : lanes) {
+        const gw_agent_spec& s = cfg->agents[a];
+        if (s.init_row >= 0 && is_static[s.init_row * cfg->cols + s.init_col]) {
+            set_err("agent %d's initial position holds a static entity (the reference raises at every reset)", a);
+            return GW_E_INVALID;
+        }
+    }
+    bool any_block = false, lane_block = false;
+    for (int a = 0; a < NE; a++) any_block |= (cfg->agents[a].kind & GW_K_BLOCKING) != 0;
+    for (int a : lanes) lane_block |= (cfg->agents[a].kind & GW_K_BLOCKING) != 0;
     if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); return GW_E_HIP; }
 
     gw_engine* g = new gw_engine();
     memset(&g->base, 0, sizeof(Params));
     g->device = device; g->E = n_envs; g->A = A; g->H = cfg->rows; g->W = cfg->cols;
     g->S = 2 * cfg->obs_range + 1; g->max_enc = max_enc;
+    for (int i = 0; i < A; i++) g->lane_ent[i] = lanes[i];
     const size_t EA = (size_t)n_envs * A;
     Params& p = g->base;
     HIPCHK(hipMalloc(&p.pos, EA * sizeof(int2)));
@@ -1525,44 +1700,119 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     HIPCHK(hipMemset(p.mt, 0, (size_t)n_envs * GW_MT_STRIDE * sizeof(uint32_t)));
     HIPCHK(hipMemset(p.steps, 0, (size_t)n_envs * sizeof(int32_t)));
     DevAgent hs[GW_MAX_AGENTS];
-    for (int a = 0; a < A; a++) {
-        const gw_agent_spec& s = cfg->agents[a];
-        hs[a].enc = s.encoding; hs[a].kind = s.kind; hs[a].init_r = s.init_row; hs[a].init_c = s.init_col;
-        hs[a].view_range = s.view_range; hs[a].move_range = s.move_range;
-        hs[a].attack_range = s.attack_range; hs[a].simul = s.simultaneous_attacks;
-        hs[a].strength = s.attack_strength; hs[a].accuracy = s.attack_accuracy;
-        hs[a].init_health = s.initial_health;
+    for (int l = 0; l < A; l++) {
+        const gw_agent_spec& s = cfg->agents[lanes[l]];
+        hs[l].enc = s.encoding; hs[l].kind = s.kind; hs[l].init_r = s.init_row; hs[l].init_c = s.init_col;
+        hs[l].view_range = s.view_range; hs[l].move_range = s.move_range;
+        hs[l].attack_range = s.attack_range; hs[l].simul = s.simultaneous_attacks;
+        hs[l].strength = s.attack_strength; hs[l].accuracy = s.attack_accuracy;
+        hs[l].init_health = s.initial_health;
     }
     HIPCHK(hipMalloc(&g->d_spec, sizeof(DevAgent) * A));
     HIPCHK(hipMemcpy(g->d_spec, hs, sizeof(DevAgent) * A, hipMemcpyHostToDevice));
     p.spec = g->d_spec;
     p.E = n_envs; p.A = A; p.H = cfg->rows; p.W = cfg->cols; p.max_enc = max_enc;
-    p.sim_kind = cfg->sim_kind; p.nav = cfg->nav_agent; p.target = cfg->target_agent;
+    p.sim_kind = cfg->sim_kind; p.nav = -1; p.target = -1;
+    for (int l = 0; l < A; l++) {
+        if (maze && lanes[l] == cfg->nav_agent) p.nav = l;
+        if (maze && lanes[l] == cfg->target_agent) p.target = l;
+    }
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
     for (int i = 0; i <= GW_MAX_ENC; i++) { p.overlap[i] = cfg->overlap[i]; p.amap[i] = cfg->attack_mapping[i]; }
     // padded cell table: border = max(view range, attack ranges); rows are
     // read as dwords, so the pitch is a multiple of 4 with slack for the
-    // over-read, plus one slack row at the end
+    // over-read, plus one slack row at the end.  Static entities are part of
+    // the template.
     int pad = cfg->obs_range;
-    for (int a = 0; a < A; a++)
-        if ((cfg->agents[a].kind & GW_K_ATTACKING) && cfg->agents[a].attack_range > pad)
-            pad = cfg->agents[a].attack_range;
+    for (int l = 0; l < A; l++)
+        if ((hs[l].kind & GW_K_ATTACKING) && hs[l].attack_range > pad) pad = hs[l].attack_range;
     p.pad = pad;
     p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 3) / 4 + 1);
     p.tbl_rows = cfg->rows + 2 * pad + 1;
     {
         const size_t tb = align16((size_t)p.tbl_rows * p.pitch);
-        uint8_t* ht = (uint8_t*)malloc(tb);
+        std::vector<uint8_t> ht(tb);
         for (size_t i = 0; i < tb; i++) {
             const int row = (int)(i / p.pitch) - pad, col = (int)(i % p.pitch) - pad;
             ht[i] = (row < 0 || row >= cfg->rows || col < 0 || col >= cfg->cols) ? CELL_OFF : 0;
         }
+        for (int a : statics) {
+            const gw_agent_spec& s = cfg->agents[a];
+            ht[(size_t)(s.init_row + pad) * p.pitch + (s.init_col + pad)] = (uint8_t)s.encoding;
+        }
         HIPCHK(hipMalloc(&g->d_tmpl, tb));
-        HIPCHK(hipMemcpy(g->d_tmpl, ht, tb, hipMemcpyHostToDevice));
-        free(ht);
+        HIPCHK(hipMemcpy(g->d_tmpl, ht.data(), tb, hipMemcpyHostToDevice));
         p.tbl_tmpl = g->d_tmpl;
+    }
+    // free cells (PositionState lists never hold a static cell: every list
+    // loses it when the static entity is placed, before any draw)
+    p.n_free = HW - (int)statics.size();
+    if (!statics.empty()) {
+        std::vector<uint16_t> fc(p.n_free + HW);
+        std::vector<uint32_t> sb((HW + 31) / 32, 0u);
+        int k = 0;
+        for (int c = 0; c < HW; c++) {
+            fc[p.n_free + c] = (uint16_t)k;
+            if (is_static[c]) sb[c >> 5] |= 1u << (c & 31);
+            else fc[k++] = (uint16_t)c;
+        }
+        HIPCHK(hipMalloc(&g->d_free, fc.size() * 2));
+        HIPCHK(hipMemcpy(g->d_free, fc.data(), fc.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&g->d_static_bits, sb.size() * 4));
+        HIPCHK(hipMemcpy(g->d_static_bits, sb.data(), sb.size() * 4, hipMemcpyHostToDevice));
+        p.free_cell = g->d_free;
+        p.cell_free = g->d_free + p.n_free;
+        p.static_bits = g->d_static_bits;
+    }
+    for (int a : statics) p.static_encs |= 1u << cfg->agents[a].encoding;
+    // blocking: shadow LUT for every range, static masks for the ranges in use
+    p.blockers = any_block;
+    p.lane_blockers = lane_block;
+    for (int r = 0; r <= GW_MAX_RANGE; r++) p.smask_off[r] = -1;
+    if (any_block) {
+        std::vector<uint32_t> lut;
+        for (int r = 0; r <= GW_MAX_RANGE; r++) {
+            p.shadow_off[r] = (int)lut.size();
+            const int D = 2 * r + 1, mw = mask_words(r);
+            lut.resize(lut.size() + (size_t)D * D * mw);
+            for (int dr = -r; dr <= r; dr++)
+                for (int dc = -r; dc <= r; dc++)
+                    host_shadow(r, dr, dc, lut.data() + p.shadow_off[r] + ((dr + r) * D + (dc + r)) * mw);
+        }
+        HIPCHK(hipMalloc(&g->d_shadow, lut.size() * 4));
+        HIPCHK(hipMemcpy(g->d_shadow, lut.data(), lut.size() * 4, hipMemcpyHostToDevice));
+        p.shadow = g->d_shadow;
+        bool used[GW_MAX_RANGE + 1] = {};
+        for (int l = 0; l < A; l++) {
+            if (hs[l].kind & GW_K_GRID_OBSERVER) used[cfg->obs_range] = true;
+            if (hs[l].kind & GW_K_ATTACKING) used[hs[l].attack_range] = true;
+        }
+        std::vector<int> sblock;
+        for (int a : statics) if (cfg->agents[a].kind & GW_K_BLOCKING) sblock.push_back(a);
+        std::vector<uint32_t> sm;
+        for (int r = 0; r <= GW_MAX_RANGE && !sblock.empty(); r++) {
+            if (!used[r]) continue;
+            p.smask_off[r] = (int)sm.size();
+            const int D = 2 * r + 1, mw = mask_words(r);
+            sm.resize(sm.size() + (size_t)HW * mw, 0u);
+            for (int cell = 0; cell < HW; cell++) {
+                const int cr = cell / cfg->cols, cc = cell % cfg->cols;
+                uint32_t* dst = sm.data() + p.smask_off[r] + (size_t)cell * mw;
+                for (int a : sblock) {
+                    const int dr = cfg->agents[a].init_row - cr, dc = cfg->agents[a].init_col - cc;
+                    if (dr < -r || dr > r || dc < -r || dc > r || (dr == 0 && dc == 0)) continue;
+                    const uint32_t* src = lut.data() + p.shadow_off[r] + ((dr + r) * D + (dc + r)) * mw;
+                    for (int w = 0; w < mw; w++) dst[w] |= src[w];
+                }
+            }
+        }
+        if (!sm.empty()) {
+            HIPCHK(hipMalloc(&g->d_smask, sm.size() * 4));
+            HIPCHK(hipMemcpy(g->d_smask, sm.data(), sm.size() * 4, hipMemcpyHostToDevice));
+            p.smask = g->d_smask;
+        }
     }
     const int SS = g->S * g->S;
     g->smem_step = smem_bytes(HW, A, SS, max_enc, p.tbl_rows * p.pitch);
@@ -1578,13 +1828,22 @@ gw_status gw_destroy(gw_handle g)
     if (!g) return GW_E_INVALID;
     (void)hipFree(g->base.pos); (void)hipFree(g->base.health); (void)hipFree(g->base.flags);
     (void)hipFree(g->base.seq); (void)hipFree(g->base.mt); (void)hipFree(g->base.steps);
-    (void)hipFree(g->d_spec); (void)hipFree(g->d_tmpl);
+    (void)hipFree(g->d_spec); (void)hipFree(g->d_tmpl); (void)hipFree(g->d_free);
+    (void)hipFree(g->d_static_bits); (void)hipFree(g->d_shadow); (void)hipFree(g->d_smask);
     delete g;
     return GW_OK;
 }
 
 int32_t gw_num_envs(gw_handle g) { return g ? g->E : 0; }
 int32_t gw_obs_side(gw_handle g) { return g ? g->S : 0; }
+int32_t gw_num_lanes(gw_handle g) { return g ? g->A : 0; }
+
+gw_status gw_lane_entities(gw_handle g, int32_t* out)
+{
+    if (!g || !out) return GW_E_INVALID;
+    for (int i = 0; i < g->A; i++) out[i] = g->lane_ent[i];
+    return GW_OK;
+}
 
 gw_status gw_seed(gw_handle g, const uint32_t* seeds, void* stream)
 {

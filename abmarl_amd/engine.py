@@ -37,12 +37,18 @@ class GridWorldEngine:
         self.device = torch.device(device if device is not None else 'cuda')
         if self.device.index is None:
             self.device = torch.device('cuda', torch.cuda.current_device())
-        self.E, self.A, self.S = int(n_envs), compiled.n_agents, compiled.obs_side
+        self.E, self.S = int(n_envs), compiled.obs_side
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_create(C.cast(C.byref(compiled.cfg), C.c_void_p), self.E,
                                            self.device.index, C.byref(h)), 'gw_create')
         self.h = h
+        # per-env arrays are per lane; static entities (never move / act /
+        # die, overlap nothing) live in the engine's cell template
+        self.A = int(self.L.gw_num_lanes(h))
+        ents = (C.c_int32 * self.A)()
+        _native.check(self.L.gw_lane_entities(h, ents), 'gw_lane_entities')
+        self.lane_entities = np.array(ents[:], dtype=np.int64)
         dev = self.device
         E, A, S = self.E, self.A, self.S
         self.obs = torch.full((E, A, S, S), -2, dtype=torch.int32, device=dev)

@@ -1,2 +1,3 @@
 from abmarl_amd.examples.team_battle import BattleAgent, TeamBattleSim  # noqa: F401
 from abmarl_amd.examples.multi_corridor import MultiCorridor  # noqa: F401
+from abmarl_amd.examples.maze_navigation import MazeNavigationAgent, MazeNavigationSim  # noqa: F401

@@ -25,7 +25,12 @@ class DictRuntime:
         self.index = {aid: i for i, aid in enumerate(self.ids)}
         self.eng = GridWorldEngine(compiled, 1, device=device, seeds=[0])
         self.dev = self.eng.device
-        A = len(self.ids)
+        # engine arrays are per lane; static entities (walls: never move, act
+        # or die, overlap nothing) have no lane (gw_engine.h "Entities and lanes")
+        self.lanes = self.eng.lane_entities
+        self.lane_of = np.full(len(self.ids), -1, np.int64)
+        self.lane_of[self.lanes] = np.arange(len(self.lanes))
+        A = len(self.lanes)
         self.obs = np.full((A, self.cc.obs_side, self.cc.obs_side), -2, np.int32)
         self.reward = np.zeros(A)
         self.done = np.ones(A, np.uint8)
@@ -56,10 +61,15 @@ class DictRuntime:
         flags = host['flags'][0]
         self.live = (flags & _abi.FLAG_LIVE) != 0
         for i, agent in enumerate(self.sim.agents.values()):
-            agent.position = host['pos'][0, i].astype(int)
+            k = self.lane_of[i]
+            if k < 0:                      # static entity: at its initial position
+                agent.position = np.array(agent.initial_position, dtype=int)
+                agent._active = True
+                continue
+            agent.position = host['pos'][0, k].astype(int)
             if isinstance(agent, HealthAgent):
-                agent._health = float(host['health'][0, i])
-            agent._active = bool(flags[i] & _abi.FLAG_ACTIVE)
+                agent._health = float(host['health'][0, k])
+            agent._active = bool(flags[k] & _abi.FLAG_ACTIVE)
 
     # -------------------------------------------------------------- protocol
     def reset(self):
@@ -78,14 +88,14 @@ class DictRuntime:
         if order != sorted(order):
             raise NotImplementedError(
                 "the engine processes actions in agents-dict order; got a different order")
-        act = np.zeros((1, len(self.ids), _abi.GW_ACT_DIM), np.int32)
+        act = np.zeros((1, len(self.lanes), _abi.GW_ACT_DIM), np.int32)
         act[0, :, 2] = -1                      # not in action_dict: does not act
         for aid, a in action_dict.items():
-            i = self.index[aid]
-            assert self.live[i], "Received an action for an agent that is already done."
+            k = self.lane_of[self.index[aid]]
+            assert k >= 0 and self.live[k], "Received an action for an agent that is already done."
             mv = a.get('move', (0, 0)) if isinstance(a, dict) else (0, 0)
-            act[0, i, 0:2] = np.asarray(mv, dtype=np.int64)
-            act[0, i, 2] = int(a.get('attack', 0)) if isinstance(a, dict) else 0
+            act[0, k, 0:2] = np.asarray(mv, dtype=np.int64)
+            act[0, k, 2] = int(a.get('attack', 0)) if isinstance(a, dict) else 0
         self._push_rng()
         obs, rew, done, all_done = self.eng.step(torch.as_tensor(act, device=self.dev))
         self.obs = obs[0].cpu().numpy()
@@ -99,19 +109,24 @@ class DictRuntime:
         if not self.observes[i]:
             return {}
         s = self.sides[i]
-        return {self.key: self.obs[i, :s, :s].astype(int)}
+        return {self.key: self.obs[self.lane_of[i], :s, :s].astype(int)}
 
     def get_reward(self, agent_id):
-        i = self.index[agent_id]
-        r = float(self.reward[i])
-        self.reward[i] = 0.0
+        k = self.lane_of[self.index[agent_id]]
+        if k < 0:
+            return 0.0
+        r = float(self.reward[k])
+        self.reward[k] = 0.0
         return r
 
     def get_done(self, agent_id):
-        return bool(self.done[self.index[agent_id]])
+        k = self.lane_of[self.index[agent_id]]
+        return False if k < 0 else bool(self.done[k])
 
     def get_all_done(self):
         return self.all_done
 
     def done_agents(self):
-        return {aid for aid, lv in zip(self.ids, self.live) if not lv}
+        out = {self.ids[i] for i in range(len(self.ids)) if self.lane_of[i] < 0}
+        out.update(self.ids[e] for e, lv in zip(self.lanes, self.live) if not lv)
+        return out

@@ -37,6 +37,21 @@
  *     reference raises as Python exceptions are reported in err_flags[E]
  *     (GW_ERR_*); the Python facade maps them back to the same exception types.
  *   - No torch / HIP types appear in the signatures: streams are void*.
+ *
+ * Entities and lanes
+ *   gw_config.agents lists every entity of the simulation (agents-dict order,
+ *   up to GW_MAX_ENTITIES).  gw_create splits them in two:
+ *     static entities: no Observing/Acting/GridObserver/Moving/Attacking/Health
+ *       mixin, an initial_position, an encoding that overlaps nothing and that
+ *       no attack_mapping names (e.g. the maze walls of
+ *       examples/rllib_maze_navigation.py).  They never move, die, act or
+ *       observe, and no other entity can share their cell, so they live in
+ *       the per-config cell-table template (and block sight when blocking);
+ *     lanes: every other entity, at most GW_MAX_AGENTS (one wavefront lane
+ *       each).
+ *   Every per-entity array below ([E][A]...) is indexed by LANE, A =
+ *   gw_num_lanes(h); gw_lane_entities gives the entity index of each lane.
+ *   Static entities sit at their initial position, active, in every env.
  */
 #ifndef GW_ENGINE_H
 #define GW_ENGINE_H
@@ -48,7 +63,8 @@ extern "C" {
 #endif
 
 /* ------------------------------------------------------------------ limits */
-#define GW_MAX_AGENTS   64   /* one wavefront lane per entity (engine)        */
+#define GW_MAX_AGENTS   64   /* lanes: one wavefront lane per dynamic entity  */
+#define GW_MAX_ENTITIES 4096 /* lanes + static entities                       */
 #define GW_MAX_ENC      15   /* encodings 1..15                               */
 #define GW_MAX_CELLS  4096   /* rows*cols                                     */
 #define GW_MAX_RANGE     7   /* view / attack range                           */
@@ -75,7 +91,9 @@ typedef int32_t gw_status;
 #define GW_K_MOVING        0x08u /* MovingAgent               gridworld/agent.py:147         */
 #define GW_K_ATTACKING     0x10u /* AttackingAgent            gridworld/agent.py:213         */
 #define GW_K_HEALTH        0x20u /* HealthAgent               gridworld/agent.py:172         */
-#define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75       */
+#define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75;
+                                    active blocking entities mask cells from
+                                    observers and attackers (utils.py:5-117) */
 
 /* ---------------------------------------------------------- sim programs */
 #define GW_SIM_TEAM_BATTLE  1   /* examples/sim/team_battle_example.py:33-59 */
@@ -104,7 +122,8 @@ typedef struct gw_agent_spec {
 
 typedef struct gw_config {
     int32_t  rows, cols;
-    int32_t  n_agents;             /* entities, in agents-dict order            */
+    int32_t  n_agents;             /* entities, in agents-dict order (lanes +
+                                      static entities, see "Entities and lanes") */
     int32_t  sim_kind;             /* GW_SIM_*                                  */
     /* overlap[e] bit f set <=> encoding e may share a cell with encoding f
        (already made symmetric, grid.py:53-71; missing key == empty set)       */
@@ -189,6 +208,9 @@ gw_status gw_destroy(gw_handle h);
 /* Introspection */
 int32_t     gw_num_envs(gw_handle h);
 int32_t     gw_obs_side(gw_handle h);
+int32_t     gw_num_lanes(gw_handle h);
+/* entity index (into gw_config.agents) of each lane; out: host int32[A]     */
+gw_status   gw_lane_entities(gw_handle h, int32_t* out);
 const char* gw_last_error(void);
 int32_t     gw_abi_version(void);
 

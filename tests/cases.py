@@ -4,12 +4,13 @@ import os
 
 import numpy as np
 
-from abmarl_amd.examples import TeamBattleSim
+from abmarl_amd.examples import TeamBattleSim, MazeNavigationAgent, MazeNavigationSim
 from abmarl_amd.sim.gridworld.agent import (
-    GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners']
+GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
+                'maze_file', 'maze_16']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -23,8 +24,23 @@ def load_golden(name):
     return d
 
 
+def build_maze(c):
+    """MazeNavigation as in the reference's examples/rllib_maze_navigation.py."""
+    registry = {
+        'N': lambda n: MazeNavigationAgent(id='navigator', encoding=1,
+                                           view_range=c['agent']['view_range']),
+        'T': lambda n: GridWorldAgent(id='target', encoding=3),
+        'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=2, blocking=True),
+    }
+    return MazeNavigationSim.build_sim_from_array(
+        np.array(c['maze'], dtype=object), registry, overlapping={1: {3}, 3: {1}},
+        states={'PositionState'}, observers={'PositionCenteredEncodingObserver'})
+
+
 def build_sim(c):
-    """The golden case's TeamBattle configuration, built with the host API."""
+    """The golden case's configuration, built with the host API."""
+    if c.get('kind') == 'maze':
+        return build_maze(c)
     agents = {}
     for i in range(c['n_agents']):
         kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])
@@ -32,9 +48,10 @@ def build_sim(c):
             kw['initial_position'] = np.array(c['initial_positions'][str(i)])
         if str(i) in c['initial_health']:
             kw['initial_health'] = c['initial_health'][str(i)]
+        if i in c.get('blocking', []):
+            kw['blocking'] = True
         agents[kw['id']] = Fighter(**kw)
-    return TeamBattleSim.build_sim(
-        c['rows'], c['cols'], agents=agents,
+    kwargs = dict(
         overlapping={int(k): set(v) for k, v in c['overlap'].items()},
         attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
         stacked_attacks=c['stacked_attacks'], observe_self=c['observe_self'],
@@ -42,6 +59,15 @@ def build_sim(c):
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
         dones={'OneTeamRemainingDone'}, state_order=c['state_order'])
+    if c.get('walls'):
+        arr = np.full((c['rows'], c['cols']), '_', dtype=object)
+        for r, cc in c['walls']:
+            arr[r, cc] = 'W'
+        wenc = c['wall_encoding']
+        return TeamBattleSim.build_sim_from_array(
+            arr, {'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=wenc, blocking=True)},
+            extra_agents=agents, **kwargs)
+    return TeamBattleSim.build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
 
 
 def team_battle(rows=32, cols=32, n_agents=64, n_teams=2, **kw):

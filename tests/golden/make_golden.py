@@ -28,6 +28,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = os.environ.get('ABMARL_REFERENCE', '/root/reference')
 
+# static walls for tb_walls: two bars and a few pillars
+WALLS_12 = [[2, c] for c in range(2, 6)] + [[r, 8] for r in range(5, 10)] + \
+    [[6, 3], [9, 5], [4, 10], [10, 1]]
+
 CASES = [
     # tiny grid that forces stacks, kills and episode ends
     dict(name='tb_small', rows=8, cols=8, n_agents=8, n_teams=2, n_envs=6, n_steps=120,
@@ -49,14 +53,56 @@ CASES = [
     # the reference example's layout: 24 agents, 4 teams on 4 corner cells
     dict(name='tb_corners', rows=8, cols=8, n_agents=24, n_teams=4, n_envs=3, n_steps=80,
          horizon=60, seed_base=5, corners=True),
+    # blocking: static walls (encoding 3, blocking, overlap nothing) from an
+    # array plus blocking fighters; attack range 2 so the attack mask matters
+    dict(name='tb_walls', rows=12, cols=12, n_agents=16, n_teams=2, n_envs=4, n_steps=120,
+         horizon=60, seed_base=77, walls=WALLS_12, wall_encoding=3, blocking=[0, 3, 5, 10],
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=3)),
+    # MazeNavigation on the reference's own examples/maze.txt
+    # (examples/rllib_maze_navigation.py: view 2, walls blocking)
+    dict(name='maze_file', kind='maze', maze='maze.txt', n_envs=4, n_steps=150, horizon=100,
+         seed_base=3, agent=dict(move_range=1, view_range=2)),
+    # MazeNavigation 16x16 from generate_maze (utils.py:120-212), N and T on passages
+    dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
+         horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
                      view_range=3)
 
 
+def maze_array(spec):
+    """The maze as a list of rows of characters ('W', 'N', 'T', '_')."""
+    if spec.startswith('generate:'):
+        from abmarl.sim.gridworld.utils import generate_maze
+        _, rows, cols, seed = spec.split(':')
+        np.random.seed(int(seed))
+        m = generate_maze(int(rows), int(cols))
+        free = [(r, c) for r in range(m.shape[0]) for c in range(m.shape[1]) if m[r, c] == 0]
+        out = [['W' if v else '_' for v in row] for row in m]
+        # target: the nearest passage at Chebyshev distance >= 3 from the
+        # navigator, so random walks reach it within an episode
+        nr, nc = free[0]
+        tr, tc = min((p for p in free if max(abs(p[0] - nr), abs(p[1] - nc)) >= 3),
+                     key=lambda p: (abs(p[0] - nr) + abs(p[1] - nc), p))
+        out[nr][nc], out[tr][tc] = 'N', 'T'
+        return out
+    path = os.path.join(REF, 'examples', spec)
+    return [line.split(' ') for line in open(path).read().splitlines()]
+
+
 def full_case(case):
     c = dict(case)
+    if c.get('kind') == 'maze':
+        c['maze'] = maze_array(c['maze'])
+        c.setdefault('state_order', 'position_health')
+        c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
+        c['action_seed'] = 1234 + c['seed_base']
+        return c
+    c.setdefault('kind', 'tb')
+    c.setdefault('walls', [])
+    c.setdefault('blocking', [])
     nt = c['n_teams']
     c.setdefault('overlap', {t: [t] for t in range(1, nt + 1)})
     c.setdefault('attack_mapping', {t: [u for u in range(1, nt + 1) if u != t]
@@ -79,9 +125,9 @@ def full_case(case):
     return c
 
 
-def make_actions(c):
+def make_actions(c, A):
     rng = np.random.RandomState(c['action_seed'])
-    T, E, A = c['n_steps'], c['n_envs'], c['n_agents']
+    T, E = c['n_steps'], c['n_envs']
     mr = c['agent']['move_range']
     act = np.zeros((T, E, A, 3), dtype=np.int8)
     act[..., 0:2] = rng.randint(-mr, mr + 1, size=(T, E, A, 2))
@@ -89,8 +135,27 @@ def make_actions(c):
     return act
 
 
+def build_reference_maze(c):
+    from abmarl.examples import MazeNavigationAgent, MazeNavigationSim
+    from abmarl.sim.gridworld.agent import GridWorldAgent
+    from abmarl.managers import AllStepManager
+    registry = {
+        'N': lambda n: MazeNavigationAgent(id='navigator', encoding=1,
+                                           view_range=c['agent']['view_range']),
+        'T': lambda n: GridWorldAgent(id='target', encoding=3),
+        'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=2, blocking=True),
+    }
+    sim = MazeNavigationSim.build_sim_from_array(
+        np.array(c['maze'], dtype=object), registry, overlapping={1: {3}, 3: {1}},
+        states={'PositionState'}, observers={'PositionCenteredEncodingObserver'})
+    return AllStepManager(sim)
+
+
 def build_reference_env(c):
+    if c['kind'] == 'maze':
+        return build_reference_maze(c)
     from abmarl.examples.sim.team_battle_example import TeamBattleSim
+    from abmarl.sim.gridworld.agent import GridWorldAgent
     from abmarl.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent, \
         HealthAgent
     from abmarl.sim.gridworld.state import PositionState, HealthState
@@ -106,9 +171,10 @@ def build_reference_env(c):
             kw['initial_position'] = np.array(c['initial_positions'][str(i)])
         if str(i) in c['initial_health']:
             kw['initial_health'] = c['initial_health'][str(i)]
+        if i in c['blocking']:
+            kw['blocking'] = True
         agents[kw['id']] = Fighter(**kw)
-    sim = TeamBattleSim.build_sim(
-        c['rows'], c['cols'], agents=agents,
+    kwargs = dict(
         overlapping={int(k): set(v) for k, v in c['overlap'].items()},
         attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
         stacked_attacks=c['stacked_attacks'],
@@ -117,6 +183,16 @@ def build_reference_env(c):
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
         dones={'OneTeamRemainingDone'})
+    if c['walls']:
+        arr = np.full((c['rows'], c['cols']), '_', dtype=object)
+        for r, cc in c['walls']:
+            arr[r, cc] = 'W'
+        wenc = c['wall_encoding']
+        sim = TeamBattleSim.build_sim_from_array(
+            arr, {'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=wenc, blocking=True)},
+            extra_agents=agents, **kwargs)
+    else:
+        sim = TeamBattleSim.build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
     # pin the set-ordered state components (smart.py:37)
     pos = [s for s in sim._states if isinstance(s, PositionState)][0]
     hea = [s for s in sim._states if isinstance(s, HealthState)][0]
@@ -126,10 +202,12 @@ def build_reference_env(c):
 
 def run_case(case):
     c = full_case(case)
-    T, E, A = c['n_steps'], c['n_envs'], c['n_agents']
+    T, E = c['n_steps'], c['n_envs']
     S = 2 * c['agent']['view_range'] + 1
-    act = make_actions(c)
-    ids = [f'agent{i}' for i in range(A)]
+    managers = [build_reference_env(c) for _ in range(E)]
+    ids = list(managers[0].agents.keys())        # entities, agents-dict order
+    A = len(ids)
+    act = make_actions(c, A)
 
     def obs_array(obs_dict):
         out = np.full((A, S, S), -2, dtype=np.int8)
@@ -140,7 +218,6 @@ def run_case(case):
                 ret[i] = 1
         return out, ret
 
-    managers = [build_reference_env(c) for _ in range(E)]
     rng_states = []
     obs0 = np.zeros((E, A, S, S), dtype=np.int8)
     for e in range(E):
@@ -181,7 +258,7 @@ def run_case(case):
                     out['done'][t, e, i] = int(bool(d[aid]))
                 agent = m.agents[aid]
                 out['pos'][t, e, i] = agent.position
-                out['health'][t, e, i] = agent.health
+                out['health'][t, e, i] = getattr(agent, 'health', 0.0)
                 out['active'][t, e, i] = int(agent.active)
             out['all_done'][t, e] = int(bool(d['__all__']))
             st = np.random.get_state()
@@ -195,8 +272,8 @@ def run_case(case):
             rng_states[e] = np.random.get_state()
     path = os.path.join(HERE, c['name'] + '.npz')
     np.savez_compressed(path, case=json.dumps(c), actions=act, obs0=obs0, **out)
-    print(f"{c['name']}: {T} steps x {E} envs x {A} agents, resets={int(out['reset_mask'].sum())}, "
-          f"kills={int((out['reward'] > 0.5).sum())} -> {os.path.getsize(path)} B")
+    print(f"{c['name']}: {T} steps x {E} envs x {A} entities, resets={int(out['reset_mask'].sum())}, "
+          f"kills/arrivals={int((out['reward'] > 0.5).sum())} -> {os.path.getsize(path)} B")
 
 
 def run_multicorridor(randomize=False, n_steps=60):
@@ -233,8 +310,12 @@ def main():
     import gym_stub
     gym_stub.install()
     sys.path.insert(0, REF)
+    only = sys.argv[1:]
     for case in CASES:
-        run_case(case)
+        if not only or case['name'] in only:
+            run_case(case)
+    if only:
+        return
     run_multicorridor(False)
     run_multicorridor(True)
 

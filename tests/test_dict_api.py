@@ -9,39 +9,42 @@ import pytest
 
 from abmarl_amd.managers import AllStepManager
 from abmarl_amd.external import MultiAgentWrapper
+from abmarl_amd.sim.agent_based_simulation import Agent
 from tests.cases import GOLDEN_CASES, load_golden, build_sim
 
 pytestmark = pytest.mark.gpu
 
 
-def _check_obs(d, ref, returned):
-    ids = sorted(d, key=lambda k: int(k[5:]))
-    assert [int(k[5:]) for k in ids] == list(np.nonzero(returned)[0])
-    for k in ids:
-        got = d[k]['position_centered_encoding']
-        np.testing.assert_array_equal(got, ref[int(k[5:])])
+def _check_obs(d, ref, returned, index):
+    got = sorted(d, key=index.get)
+    assert [index[k] for k in got] == list(np.nonzero(returned)[0])
+    for k in got:
+        np.testing.assert_array_equal(d[k]['position_centered_encoding'], ref[index[k]])
 
 
-@pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners'])
+@pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners', 'tb_walls',
+                                  'maze_file', 'maze_16'])
 def test_dict_api_matches_reference(name):
     g = load_golden(name)
     c = g['case']
-    A = c['n_agents']
     for e in range(min(3, c['n_envs'])):
         sim = build_sim(c)
+        ids = list(sim.agents)
+        index = {k: i for i, k in enumerate(ids)}
+        agents0 = np.array([isinstance(a, Agent) for a in sim.agents.values()])
         env = MultiAgentWrapper(AllStepManager(sim))
         np.random.seed(c['seeds'][e])
         obs = env.reset()
-        _check_obs(obs, g['obs0'][e], np.ones(A))
+        _check_obs(obs, g['obs0'][e], agents0, index)
         for t in range(g['actions'].shape[0]):
             done_agents = env.sim.done_agents
-            adict = {f'agent{i}': {'move': g['actions'][t, e, i, :2].astype(int),
-                                   'attack': int(g['actions'][t, e, i, 2])}
-                     for i in range(A) if f'agent{i}' not in done_agents}
+            adict = {k: {'move': g['actions'][t, e, i, :2].astype(int),
+                         'attack': int(g['actions'][t, e, i, 2])}
+                     for i, k in enumerate(ids) if k not in done_agents}
             o, r, d, _ = env.step(adict)
-            _check_obs(o, g['obs'][t, e], g['returned'][t, e])
+            _check_obs(o, g['obs'][t, e], g['returned'][t, e], index)
             for k, v in r.items():
-                i = int(k[5:])
+                i = index[k]
                 assert np.float64(v).view(np.uint64) == g['reward'][t, e, i].view(np.uint64), \
                     (t, k, v, g['reward'][t, e, i])
                 assert bool(d[k]) == bool(g['done'][t, e, i])
@@ -51,10 +54,10 @@ def test_dict_api_matches_reference(name):
             assert zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes()) == g['mt_crc'][t, e]
             for i, agent in enumerate(sim.agents.values()):
                 np.testing.assert_array_equal(agent.position, g['pos'][t, e, i])
-                assert agent.health == g['health'][t, e, i]
+                assert getattr(agent, 'health', 0.0) == g['health'][t, e, i]
             if g['reset_mask'][t, e]:
                 ro = env.reset()
-                _check_obs(ro, g['reset_obs'][t, e], np.ones(A))
+                _check_obs(ro, g['reset_obs'][t, e], agents0, index)
 
 
 def test_batched_env_autoreset_runs():

@@ -11,12 +11,29 @@ pytestmark = pytest.mark.gpu
 
 
 class EngineRunner:
+    """The engine behind the fixture's per-ENTITY layout: lane outputs are
+    scattered to their entities; static entities (walls) read as the
+    reference reports them: obs -2 (not an observer), reward 0, done 1 (not
+    an Agent), at their initial position, active, health 0."""
+
     def __init__(self, g):
         import torch
         from abmarl_amd.engine import GridWorldEngine
         self.torch = torch
         c = g['case']
-        self.eng = GridWorldEngine(golden_config(g), c['n_envs'], seeds=c['seeds'])
+        self.cc = golden_config(g)
+        self.eng = GridWorldEngine(self.cc, c['n_envs'], seeds=c['seeds'])
+        self.NE = self.cc.n_agents
+        self.lanes = self.eng.lane_entities
+        self.E = c['n_envs']
+
+    def _ent(self, x, fill):
+        out = np.full((self.E, self.NE) + x.shape[2:], fill, dtype=x.dtype)
+        out[:, self.lanes] = x
+        return out
+
+    def lane_actions(self, actions):
+        return np.ascontiguousarray(actions[:, self.lanes])
 
     def reset(self, mask):
         t = self.torch
@@ -24,17 +41,25 @@ class EngineRunner:
         obs = self.eng.reset(mask=m)
         t.cuda.synchronize()
         assert not self.eng.err.any().item()
-        return obs.cpu().numpy()
+        return self._ent(obs.cpu().numpy(), -2)
 
     def step(self, actions):
-        a = self.torch.as_tensor(actions, device=self.eng.device).contiguous()
+        a = self.torch.as_tensor(self.lane_actions(actions), device=self.eng.device).contiguous()
         obs, rew, done, all_done = self.eng.step(a)
-        return obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), all_done.cpu().numpy()
+        return (self._ent(obs.cpu().numpy(), -2), self._ent(rew.cpu().numpy(), 0.0),
+                self._ent(done.cpu().numpy(), 1), all_done.cpu().numpy())
 
     def state(self):
         st = self.eng.get_state()
         out = {k: v.cpu().numpy() for k, v in st.items()}
         out['mt'] = out['mt'].view(np.uint32)
+        pos = np.zeros((self.E, self.NE, 2), np.int32)
+        for i, sp in enumerate(self.cc.specs):
+            pos[:, i] = (sp.init_row, sp.init_col)
+        pos[:, self.lanes] = out['pos']
+        out['pos'] = pos
+        out['health'] = self._ent(out['health'], 0.0)
+        out['flags'] = self._ent(out['flags'], 0x5)    # in grid, active
         return out
 
 
@@ -56,9 +81,12 @@ def test_engine_autoreset_matches_reference(name):
     assert (obs0 == g['obs0']).all()
     c = g['case']
     for t in range(g['actions'].shape[0]):
-        a = torch.as_tensor(g['actions'][t].astype(np.int32), device=eng.device).contiguous()
+        a = torch.as_tensor(run.lane_actions(g['actions'][t].astype(np.int32)),
+                            device=eng.device).contiguous()
         obs, rew, done, ad = eng.step_autoreset(a, horizon=c['horizon'])
-        obs, rew, done, ad = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), ad.cpu().numpy()
+        obs, rew, done = (run._ent(obs.cpu().numpy(), -2), run._ent(rew.cpu().numpy(), 0.0),
+                          run._ent(done.cpu().numpy(), 1))
+        ad = ad.cpu().numpy()
         m = g['reset_mask'][t].astype(bool)
         want = np.where(m[:, None, None, None], g['reset_obs'][t], g['obs'][t])
         assert (obs == want).all(), f"step {t}: obs"
