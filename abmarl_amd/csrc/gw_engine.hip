@@ -441,12 +441,37 @@ __device__ __forceinline__ uint8_t cell_byte(uint32_t count, int enc)
     return count == 0 ? 0 : (count == 1 ? (uint8_t)enc : (uint8_t)CELL_CROWD);
 }
 
-__device__ __forceinline__ void load_rng(const Params& p, int e, Smem& sm, Rng& rng)
+// Per-env LDS state at launch start: the MT key and (copy_tmpl) the cell
+// template + zero counts.  All global loads are issued before the first LDS
+// write, so they share one round trip (a fence would stop later loads from
+// being hoisted above it).
+__device__ __forceinline__ void load_env(const Params& p, int e, Smem& sm, Rng& rng, bool copy_tmpl)
 {
-    const uint32_t* src = p.mt + (size_t)e * GW_MT_STRIDE;
+    const uint4* src = (const uint4*)(p.mt + (size_t)e * GW_MT_STRIDE);
     const int l = lane_id();
-    for (int i = l; i < GW_MT_STRIDE / 4; i += WAVE)
-        ((uint4*)sm.key)[i] = ((const uint4*)src)[i];
+    constexpr int K16 = GW_MT_STRIDE / 4;                       // 160 uint4
+    const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
+    // indices are clamped to valid addresses and the surplus is not stored
+    // (a select between loads becomes a select between pointers -> FLAT)
+    const bool k1ok = l + WAVE < K16, k2ok = l + 2 * WAVE < K16;
+    const uint4 k0 = src[l];
+    const uint4 k1 = src[k1ok ? l + WAVE : l];
+    const uint4 k2 = src[k2ok ? l + 2 * WAVE : l];
+    const bool t0ok = copy_tmpl && l < t16, t1ok = copy_tmpl && l + WAVE < t16;
+    const uint4 t0 = p.tbl_tmpl[t0ok ? l : 0];
+    const uint4 t1 = p.tbl_tmpl[t1ok ? l + WAVE : 0];
+    uint4* key4 = (uint4*)sm.key;
+    key4[l] = k0;
+    if (k1ok) key4[l + WAVE] = k1;
+    if (k2ok) key4[l + 2 * WAVE] = k2;
+    if (copy_tmpl) {
+        uint4* tb4 = (uint4*)sm.tbl;
+        if (t0ok) tb4[l] = t0;
+        if (t1ok) tb4[l + WAVE] = t1;
+        for (int i = l + 2 * WAVE; i < t16; i += WAVE) tb4[i] = p.tbl_tmpl[i];
+        const int nw = (p.H * p.W + 3) / 4;
+        for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
+    }
     wave_sync();
     rng.key = sm.key;
     rng.pos = uni((int32_t)sm.key[MT_POS_SLOT]);
@@ -467,16 +492,19 @@ __device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, cons
 }
 
 // Build the padded byte table and the counts from the lanes' positions.
-__device__ __forceinline__ void build_tables(const Params& p, Smem& sm, const Lane& L)
+// from_template: copy the per-config template (L2-resident) and zero the
+// counts first; otherwise the caller already did (load_env) or cleared the
+// lanes' old cells of a valid table and zeroed the counts (fused reset).
+__device__ __forceinline__ void build_tables(const Params& p, Smem& sm, const Lane& L, bool from_template)
 {
     const int l = lane_id();
-    const int HW = p.H * p.W;
-    const int nw = (HW + 3) / 4;
-    // border = 0xFF, interior = 0: copy of the per-config template (L2-resident)
-    const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
-    for (int i = l; i < t16; i += WAVE) ((uint4*)sm.tbl)[i] = p.tbl_tmpl[i];
-    for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
-    wave_sync();
+    if (from_template) {
+        const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
+        for (int i = l; i < t16; i += WAVE) ((uint4*)sm.tbl)[i] = p.tbl_tmpl[i];
+        const int nw = (p.H * p.W + 3) / 4;
+        for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
+        wave_sync();
+    }
     int cell = L.r * p.W + L.c;
     if (L.in_grid) atomicAdd(&sm.cnt[cnt_word(p, cell)], 1u << (8 * (cell & 3)));
     wave_sync();
@@ -629,18 +657,31 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     wave_sync();
     STAMP(9);
 
-    // stage (int8) -> obs (int32), 4 values per lane per iteration, coalesced
+    // stage (int8) -> obs (int32), 4 values per lane per iteration, coalesced;
+    // unrolled to the compile-time bound so every LDS read is in flight
+    // before the stores
     const int total = A * SS;
     int32_t* out = p.obs + (size_t)e * total;
-    for (int i = l * 4; i < total; i += WAVE * 4) {
-        if (i + 3 < total && (((size_t)e * total + i) & 3) == 0) {
-            uint32_t w = *(const uint32_t*)(sm.stage + i);
-            int4 v = make_int4((int8_t)(w & 0xff), (int8_t)((w >> 8) & 0xff),
-                               (int8_t)((w >> 16) & 0xff), (int8_t)(w >> 24));
-            *(int4*)(out + i) = v;
-        } else {
-            for (int q = i; q < i + 4 && q < total; q++) out[q] = sm.stage[q];
+    if ((total & 3) == 0) {
+        constexpr int NIT = (GW_MAX_AGENTS * SS + 4 * WAVE - 1) / (4 * WAVE);
+        constexpr int B = NIT < 16 ? NIT : 8;                   // batch of LDS reads in flight
+        for (int k0 = 0; k0 < NIT && k0 * 4 * WAVE < total; k0 += B) {
+            uint32_t w[B];
+#pragma unroll
+            for (int k = 0; k < B; k++) {
+                const int i = ((k0 + k) * WAVE + l) * 4;
+                w[k] = i < total ? *(const uint32_t*)(sm.stage + i) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < B; k++) {
+                const int i = ((k0 + k) * WAVE + l) * 4;
+                if (i < total)
+                    *(int4*)(out + i) = make_int4((int8_t)(w[k] & 0xff), (int8_t)((w[k] >> 8) & 0xff),
+                                                  (int8_t)((w[k] >> 16) & 0xff), (int8_t)(w[k] >> 24));
+            }
         }
+    } else {
+        for (int i = l; i < total; i += WAVE) out[i] = sm.stage[i];
     }
 }
 
@@ -1195,14 +1236,24 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
 }
 
 template <int S>
-__device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr)
+__device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr,
+                                          bool fused)
 {
     constexpr int SS = S * S;
     uint32_t err = 0;
+    // fused: the LDS table holds the end-of-step grid; empty the lanes' cells
+    // (static entities stay) instead of re-reading the template
+    if (fused && L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = 0;
     const bool ok = do_reset(p, sm, rng, L, ctr, err);
     STAMP(13);
     if (ok) {
-        build_tables(p, sm, L);
+        if (fused) {
+            const int nw = (p.H * p.W + 3) / 4;      // the placement used the counts as scratch
+            wave_sync();
+            for (int i = lane_id(); i < nw; i += WAVE) sm.cnt[i] = 0u;
+            wave_sync();
+        }
+        build_tables(p, sm, L, !fused);
         observe_all<S>(p, e, sm, rng, L);
     } else {
         int32_t* out = p.obs + (size_t)e * p.A * SS;
@@ -1228,21 +1279,20 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     Smem sm = carve(smem_raw, p);
     Lane L;
     load_lane(p, e, L, valid);
-    Rng rng;
-    load_rng(p, e, sm, rng);
-    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
-    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
-
     // actions (lane = agent); attack == -1 marks "not in action_dict"
     int mr = 0, mc = 0, ak = -1;
     if (valid) {
         const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
         mr = ap[0]; mc = ap[1]; ak = ap[2];
     }
+    Rng rng;
+    load_env(p, e, sm, rng, true);
+    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
+    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
     const bool acting = valid && L.live && ak >= 0;
     const uint64_t act_mask = __ballot(acting);
     STAMP(10);
-    build_tables(p, sm, L);
+    build_tables(p, sm, L, false);
     STAMP(1);
 
     if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
@@ -1388,7 +1438,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     if (p.autoreset && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
         wave_sync();
         STAMP(12);
-        reset_env<S>(p, e, sm, rng, L, ctr);
+        reset_env<S>(p, e, sm, rng, L, ctr, true);
         STAMP(14);
     }
     store_lane(p, e, L, valid);
@@ -1415,9 +1465,9 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
     Lane L;
     load_lane(p, e, L, valid);
     Rng rng;
-    load_rng(p, e, sm, rng);
+    load_env(p, e, sm, rng, false);
     uint32_t ctr = 0;
-    reset_env<S>(p, e, sm, rng, L, ctr);
+    reset_env<S>(p, e, sm, rng, L, ctr, false);
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
 }
