@@ -12,7 +12,7 @@ GW_MAX_CELLS = 4096
 GW_MAX_RANGE = 7
 GW_ACT_DIM = 3
 GW_MT_N = 624
-GW_MT_STRIDE = 640
+GW_MT_STRIDE = 704
 
 GW_OK = 0
 GW_E_INVALID = -1

@@ -34,7 +34,8 @@
 //
 // Data layout in HBM (SoA, env-major, lane-contiguous => coalesced):
 //   pos[E][A] int2, health[E][A] f64, flags[E][A] u8, seq[E][A] u32,
-//   mt[E][640] u32 (key[624], pos @624, seq counter @625), steps[E] i32.
+//   mt[E][704] u32 (key[624], pos @624, seq counter @625, cached block base
+//   @626, 64 tempered words from it @640), steps[E] i32.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -52,6 +53,8 @@
 #define F_ACTIVE 4u
 #define MT_POS_SLOT 624
 #define MT_CTR_SLOT 625
+#define MT_CBASE_SLOT 626   // base of the cached tempered block (0xFFFFFFFF: none)
+#define MT_CACHE 640        // [64] tempered key[cbase + i]
 #define SEQ_RENORM (1u << 23)
 #define CELL_CROWD 0x80u
 #define CELL_OFF 0xFFu
@@ -82,6 +85,7 @@ struct Params {
     int32_t observe_self, stacked, no_overlap_at_reset, state_order;
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
+    int32_t pair_cap;                      // crowded (observer, cell) pairs that fit after the obs stage
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
@@ -258,19 +262,40 @@ __device__ __forceinline__ void mt_twist(uint32_t* key)
     }
 }
 
-// numpy legacy RandomState (mt19937.c): key[] lives in LDS; tempered output
-// words are cached one per lane (a 64-word block), so a draw is one
-// v_readlane; the twist is lane-parallel in chunks of 64 (every write's
-// dependency i-227 is >= 3 chunks back; i+1 is read before any lane writes).
+// numpy legacy RandomState (mt19937.c).  The 624-word key stays in HBM until
+// a draw needs it (a word outside the cached block, a twist, a reset); it is
+// then copied to LDS.  The 64 tempered words from the stream position are
+// kept per env in HBM (mt[MT_CACHE..]) and in a register, one word per lane,
+// so a draw is one v_readlane and most launches never read the key.
 struct Rng {
-    uint32_t* key;      // LDS [624]
-    uint32_t cache;     // tempered key[base + lane]
-    int pos;            // next index (wave-uniform)
-    int base;           // cached block base (wave-uniform), -1 = none
-    bool dirty;         // twisted since load
+    uint32_t* key;          // LDS [624] (valid once loaded)
+    const uint32_t* gkey;   // this env's key in HBM
+    uint32_t cache;         // tempered key[base + lane] (lane < ccount)
+    int pos;                // next index (wave-uniform)
+    int base;               // cached block base (wave-uniform), -1 = none
+    int ccount;             // valid words of the cached block
+    bool loaded;            // key copied to LDS
+    bool dirty;             // twisted since load
+
+    __device__ __forceinline__ void ensure_key()
+    {
+        if (loaded) return;
+        const int l = lane_id();
+        constexpr int N4 = GW_MT_N / 4;                     // 156 uint4
+        const uint4* src = (const uint4*)gkey;
+        const bool ok2 = l + 2 * WAVE < N4;
+        const uint4 a = src[l], b = src[l + WAVE], c = src[ok2 ? l + 2 * WAVE : l];
+        uint4* k4 = (uint4*)key;
+        k4[l] = a;
+        k4[l + WAVE] = b;
+        if (ok2) k4[l + 2 * WAVE] = c;
+        wave_sync();
+        loaded = true;
+    }
 
     __device__ __forceinline__ void twist()
     {
+        ensure_key();
         mt_twist(key);
         pos = 0;
         base = -1;
@@ -280,13 +305,15 @@ struct Rng {
     __device__ __forceinline__ uint32_t next()
     {
         if (pos == GW_MT_N) twist();
-        int b = pos & ~(WAVE - 1);
-        if (b != base) {
-            int i = b + lane_id();
+        if (!(base >= 0 && pos >= base && pos - base < ccount)) {
+            ensure_key();
+            const int b = pos & ~(WAVE - 1);
+            const int i = b + lane_id();
             cache = temper(i < GW_MT_N ? key[i] : 0u);
             base = b;
+            ccount = GW_MT_N - b < WAVE ? GW_MT_N - b : WAVE;
         }
-        uint32_t v = rl(cache, pos & (WAVE - 1));
+        uint32_t v = rl(cache, pos - base);
         pos = pos + 1;
         return v;
     }
@@ -362,7 +389,7 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
 }
 
 // LDS carve-up per wave (dynamic shared memory, 16-B aligned pieces)
-//   key  [640] u32          MT19937 state
+//   key  [624] u32          MT19937 state (loaded on demand)
 //   tbl  [tbl_rows*pitch] u8 padded cell table: 0 empty, enc single,
 //                           0x80 >= 2 occupants, 0xFF off-grid (border)
 //   cnt  [ceil(HW/4)] u32   per-cell occupant counts, packed u8
@@ -391,26 +418,26 @@ constexpr size_t JAC_WORK_BYTES = JAC_OFF_KEY2 + 4 * GW_MT_N;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline size_t work_bytes(int HW, int A, int SS, int max_enc)
+__host__ __device__ inline size_t work_bytes(int HW, int A, int S, int max_enc)
 {
     size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
-    size_t s = align16((size_t)A * SS);
+    size_t s = align16((size_t)A * S * ((S + 3) & ~3));     // observation stage [A][S][SP]
     (void)max_enc;
     if (s < w) s = w;
     return s > JAC_WORK_BYTES ? s : JAC_WORK_BYTES;
 }
 
-__host__ __device__ inline size_t smem_bytes(int HW, int A, int SS, int max_enc, int tbl_bytes)
+__host__ __device__ inline size_t smem_bytes(int HW, int A, int S, int max_enc, int tbl_bytes)
 {
-    return align16(GW_MT_STRIDE * 4) + align16((size_t)tbl_bytes) +
-           align16((size_t)((HW + 3) / 4) * 4) + work_bytes(HW, A, SS, max_enc);
+    return align16(GW_MT_N * 4) + align16((size_t)tbl_bytes) +
+           align16((size_t)((HW + 3) / 4) * 4) + work_bytes(HW, A, S, max_enc);
 }
 
 __device__ __forceinline__ Smem carve(char* base, const Params& p)
 {
     const int HW = p.H * p.W;
     Smem s;
-    s.key = (uint32_t*)base; base += align16(GW_MT_STRIDE * 4);
+    s.key = (uint32_t*)base; base += align16(GW_MT_N * 4);
     s.tbl = (uint8_t*)base; base += align16((size_t)p.tbl_rows * p.pitch);
     s.cnt = (uint32_t*)base; base += align16((size_t)((HW + 3) / 4) * 4);
     s.tcnt = (uint32_t*)base;
@@ -441,29 +468,25 @@ __device__ __forceinline__ uint8_t cell_byte(uint32_t count, int enc)
     return count == 0 ? 0 : (count == 1 ? (uint8_t)enc : (uint8_t)CELL_CROWD);
 }
 
-// Per-env LDS state at launch start: the MT key and (copy_tmpl) the cell
-// template + zero counts.  All global loads are issued before the first LDS
-// write, so they share one round trip (a fence would stop later loads from
-// being hoisted above it).
-__device__ __forceinline__ void load_env(const Params& p, int e, Smem& sm, Rng& rng, bool copy_tmpl)
+// Per-env state at launch start: the RNG position/counter/cached block and
+// (copy_tmpl) the cell template + zero counts.  All global loads are issued
+// before the first LDS write, so they share one round trip (a fence would
+// stop later loads from being hoisted above it).
+__device__ __forceinline__ void load_env(const Params& p, int e, Smem& sm, Rng& rng, uint32_t& ctr,
+                                         bool copy_tmpl)
 {
-    const uint4* src = (const uint4*)(p.mt + (size_t)e * GW_MT_STRIDE);
+    const uint32_t* mt = p.mt + (size_t)e * GW_MT_STRIDE;
     const int l = lane_id();
-    constexpr int K16 = GW_MT_STRIDE / 4;                       // 160 uint4
     const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
+    const uint32_t cw = mt[MT_CACHE + l];
+    const int pos = (int)uni(mt[MT_POS_SLOT]);
+    const uint32_t c0 = uni(mt[MT_CTR_SLOT]);
+    const uint32_t cb = uni(mt[MT_CBASE_SLOT]);
     // indices are clamped to valid addresses and the surplus is not stored
     // (a select between loads becomes a select between pointers -> FLAT)
-    const bool k1ok = l + WAVE < K16, k2ok = l + 2 * WAVE < K16;
-    const uint4 k0 = src[l];
-    const uint4 k1 = src[k1ok ? l + WAVE : l];
-    const uint4 k2 = src[k2ok ? l + 2 * WAVE : l];
     const bool t0ok = copy_tmpl && l < t16, t1ok = copy_tmpl && l + WAVE < t16;
     const uint4 t0 = p.tbl_tmpl[t0ok ? l : 0];
     const uint4 t1 = p.tbl_tmpl[t1ok ? l + WAVE : 0];
-    uint4* key4 = (uint4*)sm.key;
-    key4[l] = k0;
-    if (k1ok) key4[l + WAVE] = k1;
-    if (k2ok) key4[l + 2 * WAVE] = k2;
     if (copy_tmpl) {
         uint4* tb4 = (uint4*)sm.tbl;
         if (t0ok) tb4[l] = t0;
@@ -471,13 +494,18 @@ __device__ __forceinline__ void load_env(const Params& p, int e, Smem& sm, Rng& 
         for (int i = l + 2 * WAVE; i < t16; i += WAVE) tb4[i] = p.tbl_tmpl[i];
         const int nw = (p.H * p.W + 3) / 4;
         for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
+        wave_sync();
     }
-    wave_sync();
     rng.key = sm.key;
-    rng.pos = uni((int32_t)sm.key[MT_POS_SLOT]);
-    rng.base = -1;
-    rng.cache = 0;
+    rng.gkey = mt;
+    rng.pos = pos;
+    rng.cache = cw;
+    const bool cvalid = cb <= (uint32_t)GW_MT_N && (int)cb <= pos;
+    rng.base = cvalid ? (int)cb : -1;
+    rng.ccount = cvalid ? (GW_MT_N - (int)cb < WAVE ? GW_MT_N - (int)cb : WAVE) : 0;
+    rng.loaded = false;
     rng.dirty = false;
+    ctr = c0;
 }
 
 __device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, const Rng& rng, uint32_t ctr)
@@ -487,6 +515,12 @@ __device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, cons
     if (rng.dirty) {
         wave_sync();
         for (int i = l; i < GW_MT_N / 4; i += WAVE) ((uint4*)dst)[i] = ((const uint4*)sm.key)[i];
+    }
+    if (rng.loaded) {
+        // refresh the cached block at the new position (the key is in LDS)
+        const int i = rng.pos + l;
+        dst[MT_CACHE + l] = temper(i < GW_MT_N ? sm.key[i] : 0u);
+        if (l == 0) dst[MT_CBASE_SLOT] = (uint32_t)rng.pos;
     }
     if (l == 0) { dst[MT_POS_SLOT] = (uint32_t)rng.pos; dst[MT_CTR_SLOT] = ctr; }
 }
@@ -531,17 +565,25 @@ __device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const La
 }
 
 // ------------------------------------------------------------ observation
+// Observation stage geometry: int8 [A][S][SP], each window row padded to
+// SP = 4*ceil(S/4) bytes so a decoded table dword is written to LDS as is.
+__host__ __device__ constexpr int stage_pitch(int S) { return (S + 3) & ~3; }
+
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S>
-__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L)
+__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L,
+                                            int stamp_base = 8)
 {
+    (void)stamp_base;
     constexpr int SS = S * S;
     constexpr int R = S / 2;
-    constexpr int ND = (S + 3) / 4 + 1;       // dwords covering S bytes at any alignment
+    constexpr int NW = (S + 3) / 4;           // stage dwords per window row
+    constexpr int ND = NW + 1;                // table dwords covering S bytes at any alignment
+    constexpr int SP = stage_pitch(S);
+    constexpr int SSP = S * SP;
     const int l = lane_id();
     const int A = p.A;
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
-    bool has_ev = false;
 
     // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
     // static blockers precomputed per cell, blocking lanes from the shadow LUT
@@ -568,11 +610,14 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         }
     }
 
-    // window rows -> int8 stage: every row's dwords first (independent LDS
-    // reads), then decode; hidden cells are -2 and never draw
+    // window rows -> stage: every row's dwords first (independent LDS reads),
+    // then decoded with alignbyte and written as dwords.  Table bytes are the
+    // observation values (0 empty, enc, 0xFF = -1 off-grid); 0x80 marks a
+    // crowded cell, resolved below; hidden cells become 0xFE = -2.
+    uint32_t nev = 0;                         // crowded visible cells of this observer
     auto stage_rows = [&](auto masked) {
         constexpr bool MASKED = decltype(masked)::value;
-        int8_t* st = sm.stage + l * SS;
+        uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
         const uint32_t* t32 = (const uint32_t*)sm.tbl;
         uint32_t rows[S][ND];
         const int o0 = tbl_idx(p, L.r - R, L.c - R);
@@ -584,28 +629,29 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                 rows[wr][d] = t32[CIDX((o >> 2) + d, (p.tbl_rows * p.pitch + 3) / 4, 2)];
         }
         const int sh = o0 & 3;
+        const bool self_fix = !p.observe_self && L.in_grid;
 #pragma unroll
         for (int wr = 0; wr < S; wr++) {
 #pragma unroll
-            for (int d = 0; d + 1 < ND; d++) {
-                const uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
-                const uint32_t ev = w & 0x80808080u & ~(w << 1);
+            for (int d = 0; d < NW; d++) {
+                uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
+                if (wr == R && d == R / 4 && self_fix) {        // alone on my cell, not observing myself
+                    constexpr int bs = 8 * (R & 3);
+                    if (((w >> bs) & 0xffu) != CELL_CROWD) w &= ~(0xffu << bs);
+                }
+                if constexpr (MASKED) {
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int wc = d * 4 + b;
-                    if (wc < S) {
-                        uint32_t v = (w >> (8 * b)) & 0xffu;
-                        if (wr == R && wc == R && !p.observe_self && L.in_grid && v != CELL_CROWD)
-                            v = 0;                      // alone on my cell, not observing myself
-                        bool crowd = ((ev >> (8 * b)) & 0x80u) != 0;
-                        if constexpr (MASKED) {
-                            const int kk = wr * S + wc;
-                            if ((hid[kk >> 5] >> (kk & 31)) & 1u) { v = 0xFEu; crowd = false; }
-                        }
-                        st[wr * S + wc] = (int8_t)v;
-                        has_ev |= crowd;
+                    for (int b = 0; b < 4; b++) {
+                        const int kk = wr * S + d * 4 + b;
+                        if (d * 4 + b < S && ((hid[kk >> 5] >> (kk & 31)) & 1u))
+                            w = (w & ~(0xffu << (8 * b))) | (0xFEu << (8 * b));
                     }
                 }
+                // valid bytes of this dword (the last one of a row is padded)
+                const uint32_t vm = (S - 4 * d >= 4) ? 0x80808080u
+                                        : (0x80808080u & ((1u << (8 * (S - 4 * d))) - 1u));
+                nev += (uint32_t)__popc(w & vm & ~(w << 1));
+                st32[wr * NW + d] = w;
             }
         }
     };
@@ -614,23 +660,131 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             if (p.blockers) stage_rows(std::integral_constant<bool, true>());
             else stage_rows(std::integral_constant<bool, false>());
         } else {
-            int8_t* st = sm.stage + l * SS;
-            for (int k = 0; k < SS; k++) st[k] = -2;
+            uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
+#pragma unroll
+            for (int k = 0; k < S * NW; k++) st32[k] = 0xFEFEFEFEu;
         }
     }
     wave_sync();
-    STAMP(8);
+    STAMP(stamp_base);
 
-    // serial: crowded cells draw np.random.choice in (agent, row, col) order
-    // (observer.py:224-246)
-    uint64_t olanes = __ballot(has_ev);
+    // crowded cells draw np.random.choice in (agent, row, col) order
+    // (observer.py:224-246): one bounded draw over the cell's encodings in
+    // insertion (seq) order, without the observer when observe_self=False.
+    const uint64_t ev_lanes = __ballot(nev != 0);
+    uint32_t ev_scan = 0;
+    int P = 0;
+    if (ev_lanes && (ev_lanes & (ev_lanes - 1))) {          // two or more observers
+        ev_scan = wave_incl_scan(nev);
+        P = (int)rl(ev_scan, WAVE - 1);
+    }
+    if (P >= 6 && P <= p.pair_cap) {
+        rng.ensure_key();
+        // Parallel form: every (observer, cell) pair knows its member count
+        // up front, so the stream offset of its draw is the exclusive scan
+        // of the words the earlier pairs use (iterated to consistency, as in
+        // the reset placement); the value is the j-th member by seq.
+        uint16_t* pairs = (uint16_t*)(sm.stage + A * SSP);
+        if (nev) {
+            int q = (int)(ev_scan - nev);
+            const uint32_t* st32 = (const uint32_t*)(sm.stage + l * SSP);
+#pragma unroll
+            for (int wr = 0; wr < S; wr++) {
+#pragma unroll
+                for (int d = 0; d < NW; d++) {
+                    const uint32_t w = st32[wr * NW + d];
+                    const uint32_t vm = (S - 4 * d >= 4) ? 0x80808080u
+                                        : (0x80808080u & ((1u << (8 * (S - 4 * d))) - 1u));
+                    for (uint32_t m = w & vm & ~(w << 1); m; m &= m - 1) {
+                        const int wc = d * 4 + (int)(__builtin_ctz(m) >> 3);
+                        pairs[CIDX(q++, p.pair_cap, 20)] = (uint16_t)((l << 8) | (wr << 4) | wc);
+                    }
+                }
+            }
+        }
+        // rank of every lane inside its cell by seq (lanes in crowded cells only)
+        const int my_cell = L.r * p.W + L.c;
+        const bool in_crowd = l < A && L.in_grid && cnt_get(sm.cnt, my_cell) >= 2;
+        const uint64_t crowd_lanes = __ballot(in_crowd);
+        int my_rank = 0;
+        for (uint64_t it = crowd_lanes; it; it &= it - 1) {
+            const int m = first_lane(it);
+            const int cm = rl(my_cell, m);
+            const uint32_t sq = rl(L.seq, m);
+            my_rank += (in_crowd && cm == my_cell && sq < L.seq) ? 1 : 0;
+        }
+        wave_sync();
+        bool abort = false;
+        for (int c0 = 0; c0 < P && !abort; c0 += WAVE) {
+            const int q = c0 + l;
+            const bool act = q < P;
+            const int pv = act ? (int)pairs[q] : 0;
+            const int o = pv >> 8, pwr = (pv >> 4) & 15, pwc = pv & 15;
+            const int orr = __shfl(L.r, o), occ = __shfl(L.c, o);
+            const uint32_t oseq = __shfl(L.seq, o);
+            const bool o_in = __shfl((int)L.in_grid, o) != 0;
+            const int gr = orr - R + pwr, gc = occ - R + pwc;
+            const int gcell = gr * p.W + gc;
+            const bool self_in = !p.observe_self && o_in && orr == gr && occ == gc;
+            uint32_t n = act ? cnt_get(sm.cnt, gcell) : 1u;
+            if (self_in) n -= 1;
+            const uint32_t mx = n - 1u;
+            uint32_t mk = mx;
+            mk |= mk >> 1; mk |= mk >> 2; mk |= mk >> 4;
+            int used = (act && mx > 0) ? 1 : 0;
+            uint32_t j = 0;
+            bool past = false;
+            for (int it = 0; it <= WAVE; it++) {
+                const int st0 = (int)(wave_incl_scan((uint32_t)used) - (uint32_t)used);
+                int nu = 0;
+                j = 0;
+                past = false;
+                if (act && mx > 0) {
+                    int k = rng.pos + st0;
+                    for (;;) {
+                        if (k >= GW_MT_N) { past = true; break; }   // a twist inside: serial
+                        const uint32_t w = temper(rng.key[k]) & mk;
+                        k++;
+                        if (w <= mx) { j = w; break; }
+                    }
+                    nu = k - (rng.pos + st0);
+                }
+                const bool ch = __ballot(nu != used) != 0;
+                used = nu;
+                if (!ch) break;
+            }
+            if (__ballot(past)) { abort = true; break; }
+            // the j-th member of the cell in seq order (minus the observer)
+            int val = 0;
+            for (uint64_t it = crowd_lanes; it; it &= it - 1) {
+                const int m = first_lane(it);
+                const int cm = rl(my_cell, m);
+                const int rk = rl(my_rank, m);
+                const uint32_t sq = rl(L.seq, m);
+                const int enc = rl(L.enc, m);
+                if (act && cm == gcell && !(self_in && m == o)) {
+                    const int r2 = rk - ((self_in && oseq < sq) ? 1 : 0);
+                    if (r2 == (int)j) val = enc;
+                }
+            }
+            if (act) sm.stage[o * SSP + pwr * SP + pwc] = (int8_t)val;
+            rng.pos += (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
+            rng.base = -1;
+        }
+        wave_sync();
+        if (!abort) nev = 0;
+    }
+    // serial form (few pairs, or a twist inside the batch): whatever is
+    // still crowded in the stage, in the same order
+    uint64_t olanes = __ballot(nev != 0);
     while (olanes) {
         const int o = first_lane(olanes);
         olanes &= olanes - 1;
         const int orr = rl(L.r, o), oc = rl(L.c, o);
         for (int k0 = 0; k0 < SS; k0 += WAVE) {
             const int k = k0 + l;
-            const bool crowd = k < SS && (uint8_t)sm.stage[o * SS + k] == CELL_CROWD;
+            const int sidx = o * SSP + (k / S) * SP + k % S;
+            const bool crowd = k < SS && (uint8_t)sm.stage[sidx] == CELL_CROWD;
             uint64_t bits = __ballot(crowd);
             while (bits) {
                 const int kk = k0 + (int)__builtin_ctzll(bits);
@@ -650,38 +804,54 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                     if (rank == j) { sel = m; break; }
                 }
                 const int val = rl(L.enc, sel);
-                if (l == 0) sm.stage[o * SS + kk] = (int8_t)val;
+                if (l == 0) sm.stage[o * SSP + (kk / S) * SP + kk % S] = (int8_t)val;
             }
         }
     }
     wave_sync();
-    STAMP(9);
+    STAMP(stamp_base + 1);
 
-    // stage (int8) -> obs (int32), 4 values per lane per iteration, coalesced;
-    // unrolled to the compile-time bound so every LDS read is in flight
-    // before the stores
+    // stage (int8) -> obs (int32), 4 consecutive values per lane (lane-
+    // contiguous int4 stores).  Output m sits at stage byte m + (m/S)(SP-S);
+    // when rows are padded by one byte (S = 7, 11, 15) four consecutive
+    // outputs lie within two stage dwords: one byte-permute.
     const int total = A * SS;
     int32_t* out = p.obs + (size_t)e * total;
-    if ((total & 3) == 0) {
+    if (S >= 4 && SP - S <= 1 && (total & 3) == 0) {
         constexpr int NIT = (GW_MAX_AGENTS * SS + 4 * WAVE - 1) / (4 * WAVE);
-        constexpr int B = NIT < 16 ? NIT : 8;                   // batch of LDS reads in flight
+        constexpr int B = NIT < 7 ? NIT : 7;                    // LDS reads in flight
+        constexpr uint32_t GAP = SP - S;
         for (int k0 = 0; k0 < NIT && k0 * 4 * WAVE < total; k0 += B) {
-            uint32_t w[B];
+            uint32_t lo[B], hi[B], sel[B];
 #pragma unroll
             for (int k = 0; k < B; k++) {
-                const int i = ((k0 + k) * WAVE + l) * 4;
-                w[k] = i < total ? *(const uint32_t*)(sm.stage + i) : 0u;
+                const int m = ((k0 + k) * WAVE + l) * 4;
+                const int mm = m < total ? m : 0;
+                const int q0 = mm / S, wc0 = mm - q0 * S;
+                const int base = mm + q0 * (int)GAP;
+                const int t = S - wc0;                           // outputs left in this row
+                uint32_t sl = (uint32_t)(base & 3) * 0x01010101u + 0x03020100u;
+                if (t < 4) sl += (GAP * 0x01010101u) << (8 * t);
+                sel[k] = sl;
+                const uint32_t* src = (const uint32_t*)(sm.stage + (base & ~3));
+                lo[k] = src[0];
+                hi[k] = src[1];
             }
 #pragma unroll
             for (int k = 0; k < B; k++) {
-                const int i = ((k0 + k) * WAVE + l) * 4;
-                if (i < total)
-                    *(int4*)(out + i) = make_int4((int8_t)(w[k] & 0xff), (int8_t)((w[k] >> 8) & 0xff),
-                                                  (int8_t)((w[k] >> 16) & 0xff), (int8_t)(w[k] >> 24));
+                const int m = ((k0 + k) * WAVE + l) * 4;
+                if (m < total) {
+                    const uint32_t w = __builtin_amdgcn_perm(hi[k], lo[k], sel[k]);
+                    *(int4*)(out + m) = make_int4((int8_t)(w & 0xff), (int8_t)((w >> 8) & 0xff),
+                                                  (int8_t)((w >> 16) & 0xff), (int8_t)(w >> 24));
+                }
             }
         }
     } else {
-        for (int i = l; i < total; i += WAVE) out[i] = sm.stage[i];
+        for (int m = l; m < total; m += WAVE) {
+            const int q = m / S;
+            out[m] = sm.stage[m + q * (SP - S)];
+        }
     }
 }
 
@@ -867,6 +1037,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     L.in_grid = false;
     L.reward = 0.0;
     ctr = 0;
+    rng.ensure_key();                       // placement / health read the key directly
     const bool has_health = __ballot(valid && (L.kind & GW_K_HEALTH)) != 0;
 
     auto health_reset = [&]() {
@@ -1254,7 +1425,7 @@ __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng&
             wave_sync();
         }
         build_tables(p, sm, L, !fused);
-        observe_all<S>(p, e, sm, rng, L);
+        observe_all<S>(p, e, sm, rng, L, 26);
     } else {
         int32_t* out = p.obs + (size_t)e * p.A * SS;
         for (int i = lane_id(); i < p.A * SS; i += WAVE) out[i] = -2;
@@ -1285,9 +1456,12 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
         mr = ap[0]; mc = ap[1]; ak = ap[2];
     }
+    // epilogue counters read up front (not a dependent load at the end)
+    const int32_t steps0 = uni(p.steps[e]);
+    const uint64_t acting0 = p.acting ? p.acting[e] : 0ull;
     Rng rng;
-    load_env(p, e, sm, rng, true);
-    uint32_t ctr = uni(sm.key[MT_CTR_SLOT]);
+    uint32_t ctr;
+    load_env(p, e, sm, rng, ctr, true);
     if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
     const bool acting = valid && L.live && ak >= 0;
     const uint64_t act_mask = __ballot(acting);
@@ -1428,11 +1602,11 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     const bool any_left = __ballot(live_after) != 0;
     L.live = live_after;
     const bool all_done = all || !any_left;
-    const int32_t steps = p.steps[e] + 1;
+    const int32_t steps = steps0 + 1;
     if (l == 0) {
         p.all_done[e] = (uint8_t)all_done;
         p.steps[e] = steps;
-        if (p.acting) p.acting[e] += (uint64_t)__popcll(act_mask);
+        if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
     }
     // ---- fused auto-reset: the next episode's first observation replaces obs
     if (p.autoreset && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
@@ -1465,11 +1639,19 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
     Lane L;
     load_lane(p, e, L, valid);
     Rng rng;
-    load_env(p, e, sm, rng, false);
-    uint32_t ctr = 0;
+    uint32_t ctr;
+    load_env(p, e, sm, rng, ctr, false);
+    ctr = 0;
     reset_env<S>(p, e, sm, rng, L, ctr, false);
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
+}
+
+// a key written by the host invalidates the cached tempered block
+__global__ void invalidate_cache_kernel(uint32_t* mt, int E)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < E) mt[(size_t)e * GW_MT_STRIDE + MT_CBASE_SLOT] = 0xFFFFFFFFu;
 }
 
 __global__ void seed_kernel(uint32_t* mt, const uint32_t* seeds, int E)
@@ -1485,6 +1667,7 @@ __global__ void seed_kernel(uint32_t* mt, const uint32_t* seeds, int E)
     }
     k[MT_POS_SLOT] = GW_MT_N;
     k[MT_CTR_SLOT] = 0;
+    k[MT_CBASE_SLOT] = 0xFFFFFFFFu;
 }
 
 // Philox-4x32-10
@@ -1864,8 +2047,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             p.smask = g->d_smask;
         }
     }
-    const int SS = g->S * g->S;
-    g->smem_step = smem_bytes(HW, A, SS, max_enc, p.tbl_rows * p.pitch);
+    p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
+    g->smem_step = smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
     g->smem_reset = g->smem_step;
     if (g->smem_step > 160 * 1024) { set_err("LDS need %zu B > 160 KiB", g->smem_step); return GW_E_UNSUPPORTED; }
     HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
@@ -1966,7 +2149,11 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     if (health) HIPCHK(hipMemcpyAsync(g->base.health, health, EA * 8, hipMemcpyDeviceToDevice, st));
     if (flags) HIPCHK(hipMemcpyAsync(g->base.flags, flags, EA, hipMemcpyDeviceToDevice, st));
     if (seq) HIPCHK(hipMemcpyAsync(g->base.seq, seq, EA * 4, hipMemcpyDeviceToDevice, st));
-    if (mt) HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
+    if (mt) {
+        HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(invalidate_cache_kernel, dim3((g->E + 255) / 256), dim3(256), 0, st, g->base.mt, g->E);
+        HIPCHK(hipGetLastError());
+    }
     if (steps) HIPCHK(hipMemcpyAsync(g->base.steps, steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
     return GW_OK;
 }

@@ -70,7 +70,9 @@ extern "C" {
 #define GW_MAX_RANGE     7   /* view / attack range                           */
 #define GW_ACT_DIM       3   /* actions[e][a] = {move_row, move_col, attack}  */
 #define GW_MT_N        624   /* MT19937 state words                           */
-#define GW_MT_STRIDE   640   /* words per env in the MT state array (624 key + pos, padded) */
+#define GW_MT_STRIDE   704   /* words per env in the MT state array: key[624], pos @624,
+                                internal @625..703 (a write of the key through gw_set_state
+                                invalidates the engine's cached words)            */
 
 /* ----------------------------------------------------------- status codes */
 typedef int32_t gw_status;
@@ -187,7 +189,7 @@ gw_status gw_step_autoreset(gw_handle h, const int32_t* actions, int32_t* obs, d
      health  double[E][A]
      flags   uint8[E][A]      bit0 in-grid, bit1 live (not in done_agents), bit2 active
      seq     uint32[E][A]     placement order inside a cell (dict insertion order)
-     mt      uint32[E][GW_MT_STRIDE]  key[624], pos at [624]
+     mt      uint32[E][GW_MT_STRIDE]  key[624], pos at [624], engine-internal after
      steps   int32[E]                                                          */
 gw_status gw_get_state(gw_handle h, int32_t* pos, double* health, uint8_t* flags,
                        uint32_t* seq, uint32_t* mt, int32_t* steps, void* stream);

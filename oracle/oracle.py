@@ -9,13 +9,17 @@ import subprocess
 
 import numpy as np
 
+from abmarl_amd import _abi
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, 'build', 'libgw_oracle.so')
 
 
 def build(force=False):
-    src = os.path.join(HERE, 'gw_oracle.c')
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, 'gw_oracle.c'),
+            os.path.join(os.path.dirname(HERE), 'include', 'gw_engine.h')]
+    if force or not os.path.exists(LIB) or \
+            os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(['make', '-s', '-C', HERE])
     return LIB
 
@@ -88,7 +92,7 @@ class Oracle:
         pos = np.zeros((E, A, 2), np.int32)
         health = np.zeros((E, A), np.float64)
         flags = np.zeros((E, A), np.uint8)
-        mt = np.zeros((E, 640), np.uint32)
+        mt = np.zeros((E, _abi.GW_MT_STRIDE), np.uint32)
         steps = np.zeros(E, np.int32)
         self.L.gwo_get_state(self.h, _p(pos), _p(health), _p(flags), _p(mt), _p(steps))
         return dict(pos=pos, health=health, flags=flags, mt=mt, steps=steps)

@@ -65,7 +65,8 @@ def main():
                                         rs[:, 14] - rs[:, 13], rs[:, 6] - rs[:, 0],
                                         rs[:, 11] - rs[:, 12], rs[:, 15] - rs[:, 11],
                                         rs[:, 16], rs[:, 17], rs[:, 18], rs[:, 19],
-                                        rs[:, 20], rs[:, 21], rs[:, 22], rs[:, 23], rs[:, 24], rs[:, 25]], 1))
+                                        rs[:, 20], rs[:, 21], rs[:, 22], rs[:, 23], rs[:, 24], rs[:, 25],
+                                        rs[:, 26] - rs[:, 13], rs[:, 27] - rs[:, 26], rs[:, 14] - rs[:, 27]], 1))
     d = np.concatenate(deltas)
     tot = d.sum(1)
     print(f"per-env cycles (s_memtime ticks): median {np.median(tot):.0f} p90 "
@@ -91,6 +92,8 @@ def main():
         print(f"jacobi (median sums): words {np.median(r[:, 10]):.0f} lens {np.median(r[:, 11]):.0f} "
               f"draws {np.median(r[:, 12]):.0f} cells {np.median(r[:, 13]):.0f} commit "
               f"{np.median(r[:, 14]):.0f}; sweeps median {np.median(r[:, 15]):.0f} max {r[:, 15].max()}")
+        print(f"reset obs: tables+obs-par median {np.median(r[:, 16]):.0f}, crowded draws median "
+              f"{np.median(r[:, 17]):.0f} mean {r[:, 17].mean():.0f}, store+tail median {np.median(r[:, 18]):.0f}")
 
 
 if __name__ == '__main__':
