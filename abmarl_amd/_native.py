@@ -34,6 +34,7 @@ SIGNATURES = {
     'gw_reset': (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_step_autoreset': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    'gw_step_autoreset_next': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_set_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_random_actions': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp]),

@@ -1448,6 +1448,10 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     const bool valid = l < A;
     STAMP(0);
     Smem sm = carve(smem_raw, p);
+    // epilogue counters read up front (not a dependent load at the end)
+    const int32_t steps0 = uni(p.steps[e]);
+    const bool next_reset = p.autoreset == 2 &&
+                            (uni((uint32_t)p.all_done[e]) != 0u || (p.horizon > 0 && steps0 >= p.horizon));
     Lane L;
     load_lane(p, e, L, valid);
     // actions (lane = agent); attack == -1 marks "not in action_dict"
@@ -1456,12 +1460,27 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
         mr = ap[0]; mc = ap[1]; ak = ap[2];
     }
-    // epilogue counters read up front (not a dependent load at the end)
-    const int32_t steps0 = uni(p.steps[e]);
     const uint64_t acting0 = p.acting ? p.acting[e] : 0ull;
     Rng rng;
     uint32_t ctr;
     load_env(p, e, sm, rng, ctr, true);
+    if (next_reset) {
+        // NEXT_STEP auto-reset: the episode ended in the previous call, so
+        // this call is AllStepManager.reset for the env (actions ignored):
+        // obs = first observation, reward 0, done = not an Agent, no __all__.
+        // The LDS table holds the template (load_env), as after a step.
+        reset_env<S>(p, e, sm, rng, L, ctr, true);
+        if (valid) {
+            const size_t k = (size_t)e * A + l;
+            p.reward[k] = 0.0;
+            p.done[k] = L.live ? (uint8_t)0 : (uint8_t)1;
+        }
+        if (l == 0) p.all_done[e] = 0;
+        store_lane(p, e, L, valid);
+        store_rng(p, e, sm, rng, ctr);
+        STAMP(6);
+        return;
+    }
     if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
     const bool acting = valid && L.live && ak >= 0;
     const uint64_t act_mask = __ballot(acting);
@@ -1608,8 +1627,8 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         p.steps[e] = steps;
         if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
     }
-    // ---- fused auto-reset: the next episode's first observation replaces obs
-    if (p.autoreset && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
+    // ---- SAME_STEP auto-reset: the next episode's first observation replaces obs
+    if (p.autoreset == 1 && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
         wave_sync();
         STAMP(12);
         reset_env<S>(p, e, sm, rng, L, ctr, true);
@@ -2118,6 +2137,21 @@ gw_status gw_step_autoreset(gw_handle g, const int32_t* actions, int32_t* obs, d
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.acting = acting;
     p.autoreset = 1;
+    p.horizon = horizon;
+    p.err = err_flags;
+    HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_step_autoreset_next(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
+                                 uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
+                                 uint32_t* err_flags, void* stream)
+{
+    if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.acting = acting;
+    p.autoreset = 2;
     p.horizon = horizon;
     p.err = err_flags;
     HIPCHK(do_step(g, p, (hipStream_t)stream));

@@ -127,6 +127,21 @@ class GridWorldEngine:
         self._check_debug('gw_step_autoreset')
         return self.obs, self.reward, self.done, self.all_done
 
+    def step_autoreset_next(self, actions=None, horizon=0):
+        """NEXT_STEP auto-reset (gymnasium convention): envs whose episode
+        ended in the previous call (all_done set, or at the horizon) are reset
+        by this call — obs is their first observation, reward 0, actions
+        ignored — and every other env takes one step."""
+        a = self.actions if actions is None else actions
+        assert a.dtype == torch.int32 and a.is_contiguous() and a.shape == self.actions.shape
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_step_autoreset_next(
+                self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                _ptr(self.all_done), _ptr(self.acting), int(horizon), _ptr(self.err), _stream()),
+                'gw_step_autoreset_next')
+        self._check_debug('gw_step_autoreset_next')
+        return self.obs, self.reward, self.done, self.all_done
+
     def random_actions(self, key, step, env_offset=0, out=None):
         """Synthetic random policy (Philox, keyed by key / global env / step / agent)."""
         out = self.actions if out is None else out

@@ -4,8 +4,14 @@ Workload (BASELINE.json configs[2], the metric's config): TeamBattle 32x32,
 64 BattleAgents in 2 teams, 4096 envs per GPU (weak scaling: N GPUs run
 N x 4096 envs, sharded by global env id, no data-path collective), horizon
 200 with on-device auto-reset.  One timed "step" = random-policy actions
-(Philox kernel) + the fused AllStepManager.step kernel with in-launch
-auto-reset of finished episodes, for every env.
+(Philox kernel) + one fused AllStepManager.step launch for every env.
+
+Auto-reset (--autoreset): 'next_step' (default; gymnasium NEXT_STEP, the
+batched form of RLlib calling reset() after __all__: an env whose episode
+ended is reset by the next launch, which counts no agent-steps for it) or
+'same_step' (the reset observation is returned by the terminal step's
+launch).  Both run every reset; the line reports the chosen mode and the
+other one under "other_autoreset".
 
 Metric: agent-steps/s = sum over env-steps of the acting (not-done) agents,
 the reference's len(action_dict), over all ranks / the max
@@ -54,9 +60,10 @@ def step_bytes(E, A, S):
     return E * (A * per_slot + per_env)
 
 
-def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200):
+def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200, mode='next_step'):
     """The oracle (C port of the reference step, OpenMP over envs) on this
-    host's cores, bounded to ~`seconds` of work on a sample of the workload."""
+    host's cores, bounded to ~`seconds` of work on a sample of the workload,
+    with the same auto-reset flow as the GPU line."""
     from oracle.oracle import Oracle, lib
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
     lib().gwo_set_threads(threads)
@@ -75,13 +82,20 @@ def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200):
         act = np.zeros((E, A, 3), np.int32)
         act[..., :2] = rng.randint(-1, 2, size=(E, A, 2))
         act[..., 2] = rng.randint(0, 2, size=(E, A))
-        o.step(act, obs, rew, done, ad, acting)
-        o.reset(obs, all_done=ad, horizon=horizon)
+        if mode == 'next_step':
+            rs = (ad != 0) | (o.state()['steps'] >= horizon)
+            if rs.any():
+                o.reset(obs, mask=rs.astype(np.uint8))
+                ad[rs] = 0
+            o.step(act, obs, rew, done, ad, acting, mask=(~rs).astype(np.uint8))
+        else:
+            o.step(act, obs, rew, done, ad, acting)
+            o.reset(obs, all_done=ad, horizon=horizon)
         steps += 1
     dt = time.perf_counter() - t0
     return dict(value=float(acting.sum()) / dt, unit='agent-steps/s', cores=threads, kind='port',
-                sample=f'{envs} envs x {steps} steps (incl. action generation in numpy), '
-                       f'{dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads')
+                sample=f'{envs} envs x {steps} steps, {mode} auto-reset (incl. action generation '
+                       f'in numpy), {dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads')
 
 
 def main():
@@ -93,6 +107,7 @@ def main():
     ap.add_argument('--horizon', type=int, default=200)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--autoreset', choices=['next_step', 'same_step'], default='next_step')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -108,55 +123,63 @@ def main():
     from abmarl_amd.parallel import shard_envs, gather_episode_stats
     sim = team_battle_sim()
     cc = sim.compiled()
-    E_local = args.envs
-    first, E_local = shard_envs(E_local * world, rank, world)
-    eng = GridWorldEngine(cc, E_local, seeds=env_seeds(E_local, run=0, first_env=first))
-    A, S = cc.n_agents, cc.obs_side
-    eng.reset()
-    torch.cuda.synchronize()
-    eng.check_errors()
-
+    first, E_local = shard_envs(args.envs * world, rank, world)
     key = 0x5eed0000  # policy key shared by all ranks; global env ids make streams distinct
 
-    def one_step(t, ev=None):
-        eng.random_actions(key, t, env_offset=first)
-        if ev is not None:
-            ev[0].record()
-        eng.step_autoreset(horizon=args.horizon)
-        if ev is not None:
-            ev[1].record()
+    def run(mode):
+        """Fresh engine (same seeds), warmup, then K timed steps."""
+        eng = GridWorldEngine(cc, E_local, seeds=env_seeds(E_local, run=0, first_env=first))
+        eng.reset()
+        eng.all_done.zero_()
+        torch.cuda.synchronize()
+        eng.check_errors()
+        step = eng.step_autoreset_next if mode == 'next_step' else eng.step_autoreset
 
-    for t in range(args.warmup):
-        one_step(t)
-    torch.cuda.synchronize()
-    eng.check_errors()
+        def one_step(t, ev=None):
+            eng.random_actions(key, t, env_offset=first)
+            if ev is not None:
+                ev[0].record()
+            step(horizon=args.horizon)
+            if ev is not None:
+                ev[1].record()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    acting0 = int(eng.acting.sum().item())
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for t in range(args.steps):
-        one_step(args.warmup + t, evs[t])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    acting = int(eng.acting.sum().item()) - acting0
-    step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        for t in range(args.warmup):
+            one_step(t)
+        torch.cuda.synchronize()
+        eng.check_errors()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        acting0 = int(eng.acting.sum().item())
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(args.steps):
+            one_step(args.warmup + t, evs[t])
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        acting = int(eng.acting.sum().item()) - acting0
+        step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
+        kms = torch.tensor([step_ms], dtype=torch.float64, device=eng.device)
+        if dist:
+            acts = tot.clone(); dist.all_reduce(acts, op=dist.ReduceOp.SUM)
+            tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(kms, op=dist.ReduceOp.MAX)
+            tot = torch.stack([acts[0], tmax[1], acts[2]])
+        return eng, dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
+                         step_ms=step_ms, step_ms_max=kms[0].item())
 
-    tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
-    if dist:
-        acts = tot.clone(); dist.all_reduce(acts, op=dist.ReduceOp.SUM)
-        tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        kmax = torch.tensor([step_ms], dtype=torch.float64, device=eng.device)
-        dist.all_reduce(kmax, op=dist.ReduceOp.MAX)
-        acting_all, dt_all, envs_all, step_ms_all = acts[0].item(), tmax[1].item(), acts[2].item(), kmax[0].item()
-    else:
-        acting_all, dt_all, envs_all, step_ms_all = acting, dt, E_local, step_ms
+    other = 'same_step' if args.autoreset == 'next_step' else 'next_step'
+    eng, r = run(args.autoreset)
+    A, S = eng.A, cc.obs_side
     stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
+    del eng
+    _, r2 = run(other)
+    acting_all, dt_all, envs_all, step_ms = r['acting'], r['dt'], r['envs'], r['step_ms']
+    step_ms_all = r['step_ms_max']
 
     if rank == 0:
         value = acting_all / dt_all
@@ -180,7 +203,7 @@ def main():
             'dtype': 'int32 (positions/obs), f64 (health/reward)',
             'data': 'synthetic: Philox random-policy actions, random-init TeamBattle episodes',
             'config': {'workload': 'TeamBattle 32x32, 64 agents / 2 teams, 4096 envs per GPU, '
-                                   'horizon 200, auto-reset',
+                                   f'horizon 200, {args.autoreset} auto-reset',
                        'envs_per_gpu': E_local, 'global_envs': int(envs_all),
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
@@ -191,9 +214,14 @@ def main():
                          'kernel_ms': round(step_ms_all, 4),
                          'bytes_per_launch': nbytes},
             'episode_stats': stats,
+            'autoreset': args.autoreset,
+            'other_autoreset': {'mode': other, 'value': round(r2['acting'] / r2['dt'], 1),
+                                'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
+                                'kernel_ms': round(r2['step_ms_max'], 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds)
+            out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds, horizon=args.horizon,
+                                               mode=args.autoreset)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -184,6 +184,17 @@ gw_status gw_step_autoreset(gw_handle h, const int32_t* actions, int32_t* obs, d
                             uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
                             uint32_t* err_flags, void* stream);
 
+/* NEXT_STEP auto-reset (gymnasium vector-env convention; the batched form
+   of RLlib calling AllStepManager.reset after '__all__'): an env whose
+   previous call ended its episode — all_done[e] set on INPUT, or steps[e] >=
+   horizon (horizon > 0) — is reset by this call instead of stepped: obs =
+   the first observation of the new episode, reward 0, done 1 only for
+   entities that are not Agents, all_done 0, its actions ignored and nothing
+   added to acting.  Every other env takes one step.  all_done is in/out.    */
+gw_status gw_step_autoreset_next(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
+                                 uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
+                                 uint32_t* err_flags, void* stream);
+
 /* Snapshot / restore of the engine state (device buffers, caller-owned).
      pos     int32[E][A][2]   (row, col)
      health  double[E][A]

@@ -41,6 +41,7 @@ def lib():
         L.gwo_seed.argtypes = [vp, vp]
         L.gwo_reset.argtypes = [vp, vp, vp, C.c_int32, vp, vp]
         L.gwo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.gwo_step_masked.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
         L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
         L.gwo_mt_probe.argtypes = [C.c_uint32, C.c_int32, C.c_uint32, C.c_int32, vp]
@@ -82,10 +83,12 @@ class Oracle:
         self.L.gwo_reset(self.h, _p(mask), _p(all_done), int(horizon), _p(obs), _p(err))
         return err
 
-    def step(self, actions, obs, reward, done, all_done, acting=None):
+    def step(self, actions, obs, reward, done, all_done, acting=None, mask=None):
+        """One step of every env (or of the envs with mask[e] != 0)."""
         actions = np.ascontiguousarray(actions, dtype=np.int32)
-        self.L.gwo_step(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
-                        _p(acting))
+        mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.gwo_step_masked(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
+                               _p(acting), _p(mask))
 
     def state(self):
         E, A = self.E, self.A

@@ -74,3 +74,26 @@ def test_batched_env_autoreset_runs():
     torch.cuda.synchronize()
     assert obs.shape == (32, 8, 7, 7)
     assert int(env.engine.get_state()['steps'].max()) <= 20
+
+
+def test_batched_env_next_step_autoreset():
+    """NEXT_STEP mode through the batched env: the call after an episode end
+    returns the first observation with reward 0 and no done Agents."""
+    import torch
+    from abmarl_amd.external import BatchedMultiAgentEnv
+    g = load_golden('tb_small')
+    sim = build_sim(g['case'])
+    env = BatchedMultiAgentEnv(sim, 64, horizon=15, auto_reset='next_step')
+    env.reset()
+    prev_all = np.zeros(64, bool)
+    seen = 0
+    for t in range(80):
+        obs, rew, done, ad = env.step(env.engine.random_actions(9, t))
+        torch.cuda.synchronize()
+        r, d, a = rew.cpu().numpy(), done.cpu().numpy(), ad.cpu().numpy()
+        if prev_all.any():
+            seen += int(prev_all.sum())
+            assert (r[prev_all] == 0).all() and (d[prev_all] == 0).all() and not a[prev_all].any()
+        steps = env.engine.get_state()['steps'].cpu().numpy()
+        prev_all = (a != 0) | (steps >= 15)
+    assert seen > 64

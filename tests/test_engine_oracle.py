@@ -94,3 +94,52 @@ def test_maze_navigation_1024_envs(oracle_mod):
 def test_blocking_configs(oracle_mod, kw):
     cc = team_battle(**kw)
     _run(oracle_mod, cc, E=512, T=150, horizon=50, seed_run=7, key=9)
+
+
+def test_next_step_autoreset_4096_envs(oracle_mod):
+    """gw_step_autoreset_next on the headline config: envs whose episode ended
+    in the previous call are reset (reward 0, done only for non-Agents, actions
+    ignored), the others step; checked against the oracle doing exactly that."""
+    import torch
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    cc = team_battle()
+    E, T, horizon = 4096, 150, 60
+    seeds = env_seeds(E, run=3)
+    eng = GridWorldEngine(cc, E, seeds=seeds)
+    orc = oracle_mod.Oracle(cc, E)
+    orc.seed(seeds)
+    NE, ln = cc.n_agents, eng.lane_entities
+    o_obs = orc.new_obs()
+    orc.reset(o_obs)
+    assert (eng.reset().cpu().numpy() == o_obs[:, ln]).all()
+    eng.all_done.zero_()
+    rew = np.zeros((E, NE)); done = np.zeros((E, NE), np.uint8)
+    ad = np.zeros(E, np.uint8)
+    h_act = np.zeros((E, NE, 3), np.int32)
+    resets = 0
+    for t in range(T):
+        act = eng.random_actions(17, t)
+        h_act[:, ln] = act.cpu().numpy()
+        rs = (ad != 0) | (orc.state()['steps'] >= horizon)
+        resets += int(rs.sum())
+        if rs.any():
+            orc.reset(o_obs, mask=rs.astype(np.uint8))
+        orc.step(h_act, o_obs, rew, done, ad, mask=(~rs).astype(np.uint8))
+        live = (orc.state()['flags'] >> 1) & 1
+        rew[rs] = 0.0
+        done[rs] = 1 - live[rs]
+        ad[rs] = 0
+        obs, r, d, a = eng.step_autoreset_next(act, horizon=horizon)
+        assert (a.cpu().numpy() == ad).all(), f"step {t}: __all__"
+        assert (r.cpu().numpy().view(np.uint64) == rew[:, ln].view(np.uint64)).all(), f"step {t}: reward"
+        assert (d.cpu().numpy() == done[:, ln]).all(), f"step {t}: done"
+        g = obs.cpu().numpy()
+        bad = g != o_obs[:, ln]
+        assert not bad.any(), f"step {t}: obs mismatch at {np.argwhere(bad)[:3].tolist()}"
+    torch.cuda.synchronize()
+    assert resets > E // 2, resets
+    st = eng.get_state()
+    ost = orc.state()
+    assert (st['pos'].cpu().numpy() == ost['pos'][:, ln]).all()
+    mt = st['mt'].cpu().numpy().view(np.uint32)
+    assert (mt[:, :625] == ost['mt'][:, :625]).all(), "RNG state"

@@ -16,6 +16,6 @@ rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || { echo "TESTS FAILED r
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH FAIL; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
 if [[ "$ARGS" == *" stamps "* ]]; then
-  timeout -k 10 300 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { echo STAMPS FAIL; tail -20 gpurun_out/stamps.log; exit 1; }
+  MODE=${MODE:-same_step} HORIZON=${HORIZON:-100000} timeout -k 10 300 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { echo STAMPS FAIL; tail -20 gpurun_out/stamps.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/stamps.log
 fi

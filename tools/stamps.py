@@ -26,6 +26,7 @@ NAMES = {0: 'start', 1: 'tables', 10: 'load', 2: 'attack', 3: 'move', 4: 'cells'
 
 
 HORIZON = int(os.environ.get('HORIZON', '100000'))
+MODE = os.environ.get('MODE', 'same_step')
 
 
 def main():
@@ -37,6 +38,7 @@ def main():
     st = torch.zeros((E, 32), dtype=torch.int64, device=eng.device)
     L.gw_debug_set_stamps(eng.h, C.c_void_p(st.data_ptr()))
     eng.reset()
+    eng.all_done.zero_()
     order = [0, 10, 1, 2, 3, 4, 8, 9, 5, 6]
     deltas = []
     ends = []
@@ -47,7 +49,7 @@ def main():
         st.zero_()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        eng.step_autoreset(horizon=HORIZON)
+        (eng.step_autoreset_next if MODE == 'next_step' else eng.step_autoreset)(horizon=HORIZON)
         ev1.record()
         torch.cuda.synchronize()
         s = st.cpu().numpy()
