@@ -1193,9 +1193,43 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint32_t* key2 = (uint32_t*)(sm.stage + JAC_OFF_KEY2);
         uint32_t* hist = sm.cnt;   // rebuilt by build_tables afterwards
         const int nw = (NF + 3) >> 2;
-        int chs = 2;               // chunk of 1 << chs cells per lane
+        int chs = 4;               // chunk of 1 << chs cells per lane (>= 16)
         while ((WAVE << chs) < NF) chs++;
-        const int cw = 1 << (chs - 2);
+        const int cw4 = 1 << (chs - 4);   // uint4 per chunk (1, 2 or 4)
+        const int nw4 = (nw + 3) >> 2;
+        const uint4* h4 = (const uint4*)hist;
+        // count bytes of chunk k: the sum below byte `off` and (at) the byte
+        // at `off` (off == chunk size: the whole chunk).  One uint4 per
+        // iteration; a 1024-cell grid has one-uint4 chunks (one LDS trip).
+        auto chunk_sum = [&](int k, int off, uint32_t& at) -> uint32_t {
+            uint32_t sum = 0;
+            at = 0;
+            for (int q = 0; q < cw4; q++) {
+                const int i = k * cw4 + q;
+                const bool ok = i < nw4;
+                const uint4 v = h4[ok ? i : 0];
+                const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int b0 = (q * 4 + t) * 4;          // first chunk byte of this dword
+                    const int nb = off - b0;                  // bytes of it below `off`
+                    uint32_t m = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+                    const bool live = ok && i * 4 + t < nw;
+                    if (!live) m = 0u;
+                    sum = __builtin_amdgcn_sad_u8(d[t] & m, 0u, sum);
+                    if (live && nb >= 0 && nb < 4) at = (d[t] >> (8 * nb)) & 0xffu;
+                }
+            }
+            return sum;
+        };
+        // #cells <= c among this sweep's estimates (lt: < c)
+        auto rank_le = [&](int c, uint32_t& lt) -> uint32_t {
+            const int k = c >> chs;
+            const uint32_t base = cpa[CIDX(k, WAVE, 14)];
+            uint32_t at;
+            lt = base + chunk_sum(k, c - (k << chs), at);
+            return lt + at;
+        };
         const int pos0 = rng.pos;
         const bool crosses = pos0 + JAC_WB > GW_MT_N;
         wave_sync();
@@ -1217,18 +1251,6 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             wave_sync();
         }
         ACC_T(0, t0);
-        // #cells <= c among this sweep's estimates (lt: < c)
-        auto rank_le = [&](int c, uint32_t& lt) -> uint32_t {
-            const int k = c >> chs;
-            uint32_t sum = cpa[CIDX(k, WAVE, 14)];
-            const int wc = c >> 2;
-            for (int w = k * cw; w < wc; w++) sum = __builtin_amdgcn_sad_u8(hist[w], 0u, sum);
-            const uint32_t hw = hist[CIDX(wc, nw, 15)];
-            const int sh = 8 * (c & 3);
-            sum = __builtin_amdgcn_sad_u8(hw & ((1u << sh) - 1u), 0u, sum);
-            lt = sum;
-            return sum + ((hw >> sh) & 0xffu);
-        };
         auto lanes_upto = [&](uint32_t r) -> uint64_t {   // lanes of the r lowest cells
             if (r == 0) return 0ull;
             const uint2 t = tb[CIDX((int)r - 1, WAVE, 16)];
@@ -1290,11 +1312,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 tie = (atomicAdd(&hist[CIDX(ce0 >> 2, nw, 17)], 1u << sh) >> sh) & 0xffu;
             }
             wave_sync();
-            uint32_t csum = 0;
-            for (int w = 0; w < cw; w++) {
-                const int wi = l * cw + w;
-                if (wi < nw) csum = __builtin_amdgcn_sad_u8(hist[wi], 0u, csum);
-            }
+            uint32_t dummy;
+            const uint32_t csum = chunk_sum(l, 1 << chs, dummy);
             cpa[l] = wave_incl_scan(csum) - csum;
             wave_sync();
             if (valid) {
@@ -1469,7 +1488,13 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         // this call is AllStepManager.reset for the env (actions ignored):
         // obs = first observation, reward 0, done = not an Agent, no __all__.
         // The LDS table holds the template (load_env), as after a step.
+        // The reset is the launch's critical path: issue it ahead of the
+        // SIMD's stepping waves.
+        __builtin_amdgcn_s_setprio(3);
+        STAMP(10);
+        STAMP(12);
         reset_env<S>(p, e, sm, rng, L, ctr, true);
+        STAMP(14);
         if (valid) {
             const size_t k = (size_t)e * A + l;
             p.reward[k] = 0.0;
@@ -1629,6 +1654,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     }
     // ---- SAME_STEP auto-reset: the next episode's first observation replaces obs
     if (p.autoreset == 1 && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
+        __builtin_amdgcn_s_setprio(3);                      // the launch's critical path
         wave_sync();
         STAMP(12);
         reset_env<S>(p, e, sm, rng, L, ctr, true);

@@ -58,7 +58,8 @@ def main():
             span.append(int(s[:, 6].max() - s[:, 0].min()))
             emax.append(int((s[:, 6] - s[:, 0]).max()))
         if t >= 20:
-            d = np.stack([s[:, order[i + 1]] - s[:, order[i]] for i in range(len(order) - 1)], 1)
+            stepped = s[:, 1] != 0
+            d = np.stack([s[stepped, order[i + 1]] - s[stepped, order[i]] for i in range(len(order) - 1)], 1)
             deltas.append(d)
             ends.append(s[:, 6] - s[:, 0])
             rs = s[s[:, 12] != 0]
