@@ -21,6 +21,7 @@ GW_E_UNSUPPORTED = -3
 
 GW_ERR_NO_CELL = 1
 GW_ERR_INIT_POSITION = 2
+GW_ERR_DOUBLE_REMOVE = 4
 
 GW_K_OBSERVING = 0x01
 GW_K_ACTING = 0x02
@@ -28,10 +29,15 @@ GW_K_GRID_OBSERVER = 0x04
 GW_K_MOVING = 0x08
 GW_K_ATTACKING = 0x10
 GW_K_HEALTH = 0x20
+GW_K_PROGRAM = 0x80
 GW_K_BLOCKING = 0x40
 
 GW_SIM_TEAM_BATTLE = 1
 GW_SIM_MAZE_NAV = 2
+GW_SIM_REACH_TARGET = 3
+
+GW_ATTACK_BINARY = 0
+GW_ATTACK_SELECTIVE = 1
 
 GW_DONE_ACTIVE = 0x1
 GW_DONE_ONE_TEAM = 0x2
@@ -78,6 +84,7 @@ class Config(C.Structure):
         ("target_agent", C.c_int32),
         ("nav_agent", C.c_int32),
         ("agents", C.POINTER(AgentSpec)),
+        ("attack_kind", C.c_int32),
     ]
 
 
@@ -87,7 +94,7 @@ class CompiledConfig:
     def __init__(self, rows, cols, specs, sim_kind, overlap, attack_mapping,
                  stacked_attacks=False, observe_self=True, no_overlap_at_reset=False,
                  state_order=GW_ORDER_POSITION_HEALTH, done_kind=GW_DONE_ACTIVE,
-                 obs_range=0, target_agent=-1, nav_agent=-1):
+                 obs_range=0, target_agent=-1, nav_agent=-1, attack_kind=0):
         self.n_agents = len(specs)
         self._specs = (AgentSpec * max(1, self.n_agents))()
         for i, s in enumerate(specs):
@@ -106,10 +113,20 @@ class CompiledConfig:
         cfg.target_agent = target_agent
         cfg.nav_agent = nav_agent
         cfg.agents = C.cast(self._specs, C.POINTER(AgentSpec))
+        cfg.attack_kind = attack_kind
         self.cfg = cfg
         self.rows, self.cols = rows, cols
         self.obs_side = 2 * obs_range + 1
         self.specs = list(specs)
+        self.attack_kind = attack_kind
+
+    @property
+    def act_dim(self):
+        """gw_config_act_dim (include/gw_engine.h)."""
+        if self.attack_kind != GW_ATTACK_SELECTIVE:
+            return GW_ACT_DIM
+        r = max([s.attack_range for s in self.specs if s.kind & GW_K_ATTACKING] or [0])
+        return 2 + (2 * r + 1) ** 2
 
     def ptr(self):
         return C.byref(self.cfg)

@@ -32,7 +32,7 @@ SIGNATURES = {
     'gw_create': (_i32, [_vp, _i32, _i32, C.POINTER(_vp)]),
     'gw_seed': (_i32, [_vp, _vp, _vp]),
     'gw_reset': (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp]),
-    'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_step_autoreset': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     'gw_step_autoreset_next': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -42,6 +42,7 @@ SIGNATURES = {
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),
     'gw_num_lanes': (_i32, [_vp]),
+    'gw_act_dim': (_i32, [_vp]),
     'gw_lane_entities': (_i32, [_vp, _vp]),
     'gw_last_error': (C.c_char_p, []),
     'gw_abi_version': (_i32, []),

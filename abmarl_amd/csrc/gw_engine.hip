@@ -86,6 +86,8 @@ struct Params {
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
     int32_t pair_cap;                      // crowded (observer, cell) pairs that fit after the obs stage
+    int32_t act_dim;                       // ints per entity action (gw_config_act_dim)
+    int32_t attack_kind;                   // GW_ATTACK_*
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
@@ -984,6 +986,127 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     return true;
 }
 
+// SelectiveAttackActor._determine_attack (actor.py:689-728) for attacker a,
+// then the damage of AttackActorBaseComponent.process_action (:343-361).
+// `cells`: the attacker's row-major (2R+1)^2 attack counts (HBM, uniform).
+// Cells are visited in (r, c) order; each attacked cell's candidates (by
+// seq) draw for accuracy, then _subset_attackables picks that cell's share.
+// Returns the attack status; lane t holds attacked-list entry t.
+__device__ __forceinline__ bool attack_selective(const Params& p, Smem& sm, Rng& rng, Lane& L, int a,
+                                                 const int32_t* cells, int& nlist, int& list)
+{
+    const int l = lane_id();
+    nlist = 0;
+    list = -1;
+    const uint32_t akind = rl(L.kind, a);
+    if (!(akind & GW_K_ATTACKING)) return false;
+    const int R = rl(L.arange, a);
+    const int D = 2 * R + 1;
+    bool any = false;
+    for (int q = 0; q < D * D; q++) any |= cells[q] != 0;
+    if (!any) return false;                                 // (False, [])
+    const int ar = rl(L.r, a), ac = rl(L.c, a);
+    const double acc = rld(L.accuracy, a);
+    const uint32_t amap = rl(L.amap, a);
+    const int dr = L.r - ar, dc = L.c - ac;
+    bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
+                dr >= -R && dr <= R && dc >= -R && dc <= R;
+    const int myq = (dr + R) * D + (dc + R);
+    if (p.blockers) {                                       // attack mask (create_grid_and_mask)
+        const int mw = mask_words(R);
+        bool hidden = false;
+        if (cand && p.smask_off[R] >= 0)
+            hidden = (p.smask[p.smask_off[R] + (size_t)(ar * p.W + ac) * mw + (myq >> 5)] >> (myq & 31)) & 1u;
+        if (p.lane_blockers) {
+            for (uint64_t bl = __ballot(l < p.A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
+                const int b = first_lane(bl);
+                const int bdr = rl(L.r, b) - ar, bdc = rl(L.c, b) - ac;
+                if (bdr < -R || bdr > R || bdc < -R || bdc > R || (bdr == 0 && bdc == 0)) continue;
+                if (cand) {
+                    const uint32_t* src = p.shadow + p.shadow_off[R] + ((bdr + R) * D + (bdc + R)) * mw;
+                    hidden = hidden || ((src[myq >> 5] >> (myq & 31)) & 1u);
+                }
+            }
+        }
+        cand = cand && !hidden;
+    }
+    const uint64_t cm = __ballot(cand);
+    for (int q = 0; q < D * D && cm; q++) {
+        const int k = cells[q];
+        if (k == 0) continue;                               // no attack on this cell
+        const bool here = cand && myq == q;
+        uint64_t mm = __ballot(here);
+        if (!mm) continue;
+        // _basic_criteria in cell (seq) order: accuracy draws
+        int arank = -1;                                     // rank among this cell's accepted
+        int n = 0;
+        while (mm) {
+            uint32_t best = 0xFFFFFFFFu;
+            int j = -1;
+            for (uint64_t it = mm; it; it &= it - 1) {      // lowest seq left
+                const int m = first_lane(it);
+                const uint32_t sq = rl(L.seq, m);
+                if (sq < best) { best = sq; j = m; }
+            }
+            mm &= ~(1ull << j);
+            const double u = rng.uniform();
+            if (u > acc) continue;
+            if (l == j) arank = n;
+            n++;
+        }
+        if (n == 0) continue;
+        // _subset_attackables (actor.py:394-414)
+        int pick = -1, take;
+        if (!p.stacked && k > n) {
+            pick = l < n ? l : -1;
+            take = n;
+        } else if (p.stacked) {
+            for (int t = 0; t < k; t++) {
+                const int idx = (int)rng.interval((uint32_t)(n - 1));
+                if (l == t) pick = idx;
+            }
+            take = k;
+        } else {
+            int perm = l;                                   // permutation(n)[:k]
+            for (int i = n - 1; i >= 1; i--) {
+                const int j = (int)rng.interval((uint32_t)i);
+                const int pi = rl(perm, i), pj = rl(perm, j);
+                if (l == i) perm = pj;
+                if (l == j) perm = pi;
+            }
+            pick = l < k ? perm : -1;
+            take = k;
+        }
+        if (nlist + take > WAVE) take = WAVE - nlist;      // counts beyond the action space
+        for (int t = 0; t < take; t++) {
+            const int pr = rl(pick, t);
+            const uint64_t tm = __ballot(arank == pr && here);
+            CHECK(__popcll(tm) == 1, 9, pr, n);
+            if (l == nlist + t) list = first_lane(tm);
+        }
+        nlist += take;
+    }
+    // apply damage in list order (actor.py:353-358)
+    const double strength = rld(L.strength, a);
+    for (int t = 0; t < nlist; t++) {
+        const int b = rl(list, t);
+        if (!rlb(L.active, b)) continue;                    // already dead: skipped
+        if (l == b) {
+            double h = L.health - strength;
+            if (0.0 > h) h = 0.0;
+            if (1.0 < h) h = 1.0;
+            L.health = h;
+            L.active = h > 0.0;
+        }
+        if (!rlb(L.active, b)) {                            // grid.remove
+            const int br = rl(L.r, b), bc = rl(L.c, b);
+            if (l == b) L.in_grid = false;
+            table_remove(p, sm, L, b, br, bc);
+        }
+    }
+    return true;
+}
+
 // MoveActor.process_action, serial form (Grid.query as a ballot)
 __device__ __forceinline__ bool move_one(const Params& p, Lane& L, int a, int mr, int mc, uint32_t newseq)
 {
@@ -1476,7 +1599,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     // actions (lane = agent); attack == -1 marks "not in action_dict"
     int mr = 0, mc = 0, ak = -1;
     if (valid) {
-        const int32_t* ap = p.actions + ((size_t)e * A + l) * GW_ACT_DIM;
+        const int32_t* ap = p.actions + ((size_t)e * A + l) * p.act_dim;
         mr = ap[0]; mc = ap[1]; ak = ap[2];
     }
     const uint64_t acting0 = p.acting ? p.acting[e] : 0ull;
@@ -1587,6 +1710,68 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         wave_sync();
         if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
         wave_sync();
+    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+        // ---- attack pass (reach_the_target.py:96-108): every acting agent,
+        // dict order; only AttackingAgents attack (others return False, [])
+        const int32_t* act_e = p.actions + (size_t)e * A * p.act_dim;
+        for (uint64_t it = __ballot(acting && (L.kind & GW_K_ATTACKING)); it; it &= it - 1) {
+            const int a = first_lane(it);
+            if (!rlb(L.active, a)) continue;
+            int nlist, list;
+            const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
+                ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
+                : attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+            if (!status) continue;
+            if (nlist == 0) { if (l == a) L.reward -= 0.1; }
+            else {
+                for (int t = 0; t < nlist; t++) {
+                    const int b = rl(list, t);
+                    if (!rlb(L.active, b)) {
+                        if (l == b) L.reward -= 1.0;
+                        if (l == a) L.reward += 1.0;
+                    }
+                }
+            }
+        }
+        STAMP(2);
+        // ---- move pass (:110-121): MovingAgents in dict order; active ones
+        // move (-0.1 on failure); then any of them on the target's cell is
+        // rewarded, removed from the grid and deactivated.  Removing one the
+        // target already killed there is the reference's KeyError.
+        const int t = p.target;
+        const int tr = rl(L.r, t), tc = rl(L.c, t);         // the target never moves
+        for (uint64_t it = __ballot(acting && (L.kind & GW_K_MOVING)); it; it &= it - 1) {
+            const int a = first_lane(it);
+            if (rlb(L.active, a)) {
+                const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                if (!ok && l == a) L.reward -= 0.1;
+            }
+            if (rl(L.r, a) == tr && rl(L.c, a) == tc) {
+                if (!rlb(L.in_grid, a)) {
+                    // Grid.remove raises KeyError: the step stops here (no
+                    // further moves, no observation draws); the env needs a reset
+                    if (l == 0) {
+                        if (p.err) p.err[e] |= GW_ERR_DOUBLE_REMOVE;
+                        p.steps[e] = steps0 + 1;
+                        if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
+                    }
+                    ctr += (uint32_t)WAVE;
+                    store_lane(p, e, L, valid);
+                    store_rng(p, e, sm, rng, ctr);
+                    return;
+                }
+                if (l == a) {
+                    L.reward += 1.0;
+                    L.in_grid = false;
+                    L.active = false;
+                }
+            }
+        }
+        ctr += (uint32_t)WAVE;
+        // ---- entropy for the runners (:123-126)
+        if (acting && (L.kind & GW_K_PROGRAM)) L.reward -= 0.01;
+        // the LDS table after the passes (observation)
+        build_tables(p, sm, L, true);
     } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
         const int n = p.nav, t = p.target;
         if ((act_mask >> n) & 1) {
@@ -1618,9 +1803,17 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
 
     // ---- rewards, dones (:72-79, smart.py:101-111)
     bool dn;
+    bool only_left = false;                 // OnlyAgentLeftDone (reach_the_target.py:41-55)
     if (p.sim_kind == GW_SIM_MAZE_NAV) {
         const int n = p.nav, t = p.target;
         dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+        const int t = p.target;
+        const bool is_agent = (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
+        only_left = __popcll(__ballot(valid && is_agent && L.active)) <= 1;
+        const bool at_target = L.r == rl(L.r, t) && L.c == rl(L.c, t);
+        // runners: ActiveDone or TargetDone; the target: OnlyAgentLeftDone (:144-150)
+        dn = (L.kind & GW_K_PROGRAM) ? (!L.active || at_target) : only_left;
     } else {
         dn = !L.active;
     }
@@ -1634,6 +1827,8 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     bool all;
     if (p.sim_kind == GW_SIM_MAZE_NAV) {
         all = dn;
+    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+        all = only_left;
     } else {
         all = true;
         // static entities are agents too, always active (done.py:49-56,147-153)
@@ -1730,20 +1925,34 @@ __device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
 }
 
 __global__ void random_actions_kernel(const DevAgent* spec, int E, int A, uint64_t key,
-                                      uint32_t step, uint32_t env_offset, int32_t* actions)
+                                      uint32_t step, uint32_t env_offset, int32_t* actions,
+                                      int act_dim, int attack_kind)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E * A) return;
     const int e = i / A, a = i % A;
     const DevAgent s = spec[a];
-    uint4 r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED),
-                     make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
+    const uint2 k2 = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+    uint4 r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED), k2);
     const int m = s.move_range;
     const uint32_t span = (uint32_t)(2 * m + 1);
-    int32_t* o = actions + (size_t)i * GW_ACT_DIM;
+    int32_t* o = actions + (size_t)i * act_dim;
     o[0] = (s.kind & GW_K_MOVING) ? (int32_t)(r.x % span) - m : 0;
     o[1] = (s.kind & GW_K_MOVING) ? (int32_t)(r.y % span) - m : 0;
-    o[2] = (s.kind & GW_K_ATTACKING) ? (int32_t)(r.z % (uint32_t)(s.simul + 1)) : 0;
+    const uint32_t na = (uint32_t)(s.simul + 1);
+    if (attack_kind != GW_ATTACK_SELECTIVE) {
+        o[2] = (s.kind & GW_K_ATTACKING) ? (int32_t)(r.z % na) : 0;
+        return;
+    }
+    // SelectiveAttackActor: Box(0, simultaneous, (2r+1, 2r+1)) per cell
+    const int d = 2 * s.attack_range + 1;
+    const int nc = (s.kind & GW_K_ATTACKING) ? d * d : 0;
+    for (int q = 0; q < act_dim - 2; q++) {
+        if ((q & 3) == 0 && q > 0)
+            r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED + (uint32_t)(q >> 2)), k2);
+        const uint32_t w = (q & 3) == 0 ? r.z : (q & 3) == 1 ? r.w : (q & 3) == 2 ? r.x : r.y;
+        o[2 + q] = q < nc ? (int32_t)(w % na) : 0;
+    }
 }
 
 }  // namespace
@@ -1894,7 +2103,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         set_err("obs_range %d > %d", cfg->obs_range, GW_MAX_RANGE);
         return GW_E_UNSUPPORTED;
     }
-    if (cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_MAZE_NAV) {
+    if (cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_MAZE_NAV &&
+        cfg->sim_kind != GW_SIM_REACH_TARGET) {
         set_err("unknown sim_kind %d", cfg->sim_kind);
         return GW_E_INVALID;
     }
@@ -1914,9 +2124,28 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         if (s.encoding > max_enc) max_enc = s.encoding;
     }
     const bool maze = cfg->sim_kind == GW_SIM_MAZE_NAV;
+    const bool rtt = cfg->sim_kind == GW_SIM_REACH_TARGET;
     if (maze && (cfg->nav_agent < 0 || cfg->nav_agent >= NE || cfg->target_agent < 0 || cfg->target_agent >= NE)) {
         set_err("maze navigation needs nav_agent/target_agent");
         return GW_E_INVALID;
+    }
+    if (rtt && (cfg->target_agent < 0 || cfg->target_agent >= NE)) {
+        set_err("reach-the-target needs target_agent");
+        return GW_E_INVALID;
+    }
+    if (cfg->attack_kind != GW_ATTACK_BINARY && cfg->attack_kind != GW_ATTACK_SELECTIVE) {
+        set_err("unknown attack_kind %d", cfg->attack_kind);
+        return GW_E_INVALID;
+    }
+    if (cfg->attack_kind == GW_ATTACK_SELECTIVE) {
+        for (int a = 0; a < NE; a++) {
+            const gw_agent_spec& s = cfg->agents[a];
+            const int d = 2 * s.attack_range + 1;
+            if ((s.kind & GW_K_ATTACKING) && d * d * (s.simultaneous_attacks > 0 ? s.simultaneous_attacks : 1) > WAVE) {
+                set_err("agent %d: (2r+1)^2 * simultaneous_attacks > %d attacked slots", a, WAVE);
+                return GW_E_UNSUPPORTED;
+            }
+        }
     }
     // ---- entities -> static entities | lanes (gw_engine.h "Entities and lanes")
     uint32_t attacked = 0, overlapped = 0;
@@ -1929,7 +2158,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         const bool st = !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
                         cfg->overlap[s.encoding] == 0 && !((overlapped >> s.encoding) & 1u) &&
                         !((attacked >> s.encoding) & 1u) &&
-                        !(maze && (a == cfg->nav_agent || a == cfg->target_agent));
+                        !((maze || rtt) && (a == cfg->nav_agent || a == cfg->target_agent));
         (st ? statics : lanes).push_back(a);
     }
     const int A = (int)lanes.size();
@@ -1993,8 +2222,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.sim_kind = cfg->sim_kind; p.nav = -1; p.target = -1;
     for (int l = 0; l < A; l++) {
         if (maze && lanes[l] == cfg->nav_agent) p.nav = l;
-        if (maze && lanes[l] == cfg->target_agent) p.target = l;
+        if ((maze || rtt) && lanes[l] == cfg->target_agent) p.target = l;
     }
+    p.act_dim = gw_config_act_dim(cfg);
+    p.attack_kind = cfg->attack_kind;
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
@@ -2115,6 +2346,7 @@ gw_status gw_destroy(gw_handle g)
 int32_t gw_num_envs(gw_handle g) { return g ? g->E : 0; }
 int32_t gw_obs_side(gw_handle g) { return g ? g->S : 0; }
 int32_t gw_num_lanes(gw_handle g) { return g ? g->A : 0; }
+int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
 
 gw_status gw_lane_entities(gw_handle g, int32_t* out)
 {
@@ -2143,12 +2375,13 @@ gw_status gw_reset(gw_handle g, const uint8_t* mask, const uint8_t* all_done, in
 }
 
 gw_status gw_step(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
-                  uint8_t* done, uint8_t* all_done, uint64_t* acting, void* stream)
+                  uint8_t* done, uint8_t* all_done, uint64_t* acting, uint32_t* err_flags, void* stream)
 {
     if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.acting = acting;
+    p.err = err_flags;
     p.autoreset = 0;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
     return GW_OK;
@@ -2240,7 +2473,8 @@ gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t e
     if (!g || !actions) return GW_E_INVALID;
     const int n = g->E * g->A;
     hipLaunchKernelGGL(random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, env_offset, actions);
+                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, env_offset, actions,
+                       g->base.act_dim, g->base.attack_kind);
     HIPCHK(hipGetLastError());
     return GW_OK;
 }

@@ -57,7 +57,8 @@ class GridWorldEngine:
         self.all_done = torch.zeros((E,), dtype=torch.uint8, device=dev)
         self.err = torch.zeros((E,), dtype=torch.int32, device=dev)
         self.acting = torch.zeros((E,), dtype=torch.int64, device=dev)
-        self.actions = torch.zeros((E, A, _abi.GW_ACT_DIM), dtype=torch.int32, device=dev)
+        self.act_dim = int(self.L.gw_act_dim(self.h))
+        self.actions = torch.zeros((E, A, self.act_dim), dtype=torch.int32, device=dev)
         self._dbg = None
         if _native.VARIANT == 'checks':
             self._dbg = torch.zeros(16, dtype=torch.int32, device=dev)
@@ -109,7 +110,7 @@ class GridWorldEngine:
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
                                          _ptr(self.done), _ptr(self.all_done), _ptr(self.acting),
-                                         _stream()), 'gw_step')
+                                         _ptr(self.err), _stream()), 'gw_step')
         self._check_debug('gw_step')
         return self.obs, self.reward, self.done, self.all_done
 
@@ -160,6 +161,10 @@ class GridWorldEngine:
         if (err & _abi.GW_ERR_INIT_POSITION).any():
             e = int(np.nonzero(err & _abi.GW_ERR_INIT_POSITION)[0][0])
             raise AssertionError(f"Initial cell not available (env {e})")
+        if (err & _abi.GW_ERR_DOUBLE_REMOVE).any():
+            e = int(np.nonzero(err & _abi.GW_ERR_DOUBLE_REMOVE)[0][0])
+            raise KeyError(f"Grid.remove of an agent no longer in the grid (env {e}; "
+                           f"reach_the_target.py:118-120)")
 
     # ------------------------------------------------------------ state
     def get_state(self):

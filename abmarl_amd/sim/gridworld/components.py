@@ -125,6 +125,15 @@ class BinaryAttackActor(AttackActorBaseComponent):
         agent.null_action[self.key] = 0
 
 
+class SelectiveAttackActor(AttackActorBaseComponent):
+    """actor.py:659-728: Box(0, simultaneous_attacks, (2r+1, 2r+1)) attacks per cell."""
+
+    def _assign_space(self, agent):
+        d = 2 * agent.attack_range + 1
+        agent.action_space[self.key] = Box(0, agent.simultaneous_attacks, (d, d), int)
+        agent.null_action[self.key] = np.zeros((d, d), dtype=int)
+
+
 # -------------------------------------------------------------- observers
 class ObserverBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
     """observer.py:13-52."""

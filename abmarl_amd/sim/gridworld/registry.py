@@ -4,7 +4,7 @@ Only components the engine can execute are registered; ``register`` of any
 other subclass raises, because the fused step cannot run arbitrary Python.
 """
 from abmarl_amd.sim.gridworld.components import (
-    ActorBaseComponent, MoveActor, BinaryAttackActor,
+    ActorBaseComponent, MoveActor, BinaryAttackActor, SelectiveAttackActor,
     DoneBaseComponent, ActiveDone, OneTeamRemainingDone,
     ObserverBaseComponent, PositionCenteredEncodingObserver,
     StateBaseComponent, PositionState, HealthState,
@@ -18,7 +18,7 @@ _subclass_check_mapping = {
 }
 
 _registered_components = {
-    'actor': {MoveActor, BinaryAttackActor},
+    'actor': {MoveActor, BinaryAttackActor, SelectiveAttackActor},
     'done': {ActiveDone, OneTeamRemainingDone},
     'observer': {PositionCenteredEncodingObserver},
     'state': {PositionState, HealthState},

@@ -74,6 +74,7 @@ class DictRuntime:
     # -------------------------------------------------------------- protocol
     def reset(self):
         self._push_rng()
+        self.eng.err.zero_()
         obs = self.eng.reset()
         self.eng.check_errors()
         self.obs = obs[0].cpu().numpy()
@@ -88,21 +89,25 @@ class DictRuntime:
         if order != sorted(order):
             raise NotImplementedError(
                 "the engine processes actions in agents-dict order; got a different order")
-        act = np.zeros((1, len(self.lanes), _abi.GW_ACT_DIM), np.int32)
+        act = np.zeros((1, len(self.lanes), self.eng.act_dim), np.int32)
         act[0, :, 2] = -1                      # not in action_dict: does not act
         for aid, a in action_dict.items():
             k = self.lane_of[self.index[aid]]
             assert k >= 0 and self.live[k], "Received an action for an agent that is already done."
-            mv = a.get('move', (0, 0)) if isinstance(a, dict) else (0, 0)
-            act[0, k, 0:2] = np.asarray(mv, dtype=np.int64)
-            act[0, k, 2] = int(a.get('attack', 0)) if isinstance(a, dict) else 0
+            a = a if isinstance(a, dict) else {}
+            act[0, k, 0:2] = np.asarray(a.get('move', (0, 0)), dtype=np.int64)
+            at = np.asarray(a.get('attack', 0), dtype=np.int64).reshape(-1)
+            act[0, k, 2] = 0
+            act[0, k, 2:2 + at.size] = at      # binary: one int; selective: (2r+1)^2 cells
         self._push_rng()
+        self.eng.err.zero_()
         obs, rew, done, all_done = self.eng.step(torch.as_tensor(act, device=self.dev))
         self.obs = obs[0].cpu().numpy()
         self.reward = rew[0].cpu().numpy().copy()
         self.done = done[0].cpu().numpy().copy()
         self.all_done = bool(all_done[0].item())
         self._pull()
+        self.eng.check_errors()                # e.g. ReachTheTarget's double remove -> KeyError
 
     def get_obs(self, agent_id):
         i = self.index[agent_id]

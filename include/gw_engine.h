@@ -68,7 +68,8 @@ extern "C" {
 #define GW_MAX_ENC      15   /* encodings 1..15                               */
 #define GW_MAX_CELLS  4096   /* rows*cols                                     */
 #define GW_MAX_RANGE     7   /* view / attack range                           */
-#define GW_ACT_DIM       3   /* actions[e][a] = {move_row, move_col, attack}  */
+#define GW_ACT_DIM       3   /* binary-attack sims: actions[e][a] = {move_row, move_col, attack};
+                                see gw_act_dim() for the general width                */
 #define GW_MT_N        624   /* MT19937 state words                           */
 #define GW_MT_STRIDE   704   /* words per env in the MT state array: key[624], pos @624,
                                 internal @625..703 (a write of the key through gw_set_state
@@ -84,6 +85,8 @@ typedef int32_t gw_status;
 /* per-env error flags (err_flags[e], OR-ed) */
 #define GW_ERR_NO_CELL        1u  /* PositionState: RuntimeError "Could not find a cell"  state.py:158-162 */
 #define GW_ERR_INIT_POSITION  2u  /* PositionState: AssertionError initial cell taken     state.py:147-149 */
+#define GW_ERR_DOUBLE_REMOVE  4u  /* ReachTheTarget: KeyError, Grid.remove of an agent the target
+                                     already killed on its own cell (reach_the_target.py:118-120) */
 
 /* ------------------------------------------------------------ agent kinds */
 /* bit flags describing which reference mixins an entity derives from        */
@@ -93,6 +96,8 @@ typedef int32_t gw_status;
 #define GW_K_MOVING        0x08u /* MovingAgent               gridworld/agent.py:147         */
 #define GW_K_ATTACKING     0x10u /* AttackingAgent            gridworld/agent.py:213         */
 #define GW_K_HEALTH        0x20u /* HealthAgent               gridworld/agent.py:172         */
+#define GW_K_PROGRAM       0x80u /* the sim program's own agent class (ReachTheTarget:
+                                    RunningAgent, reach_the_target.py:75-81)        */
 #define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75;
                                     active blocking entities mask cells from
                                     observers and attackers (utils.py:5-117) */
@@ -100,6 +105,11 @@ typedef int32_t gw_status;
 /* ---------------------------------------------------------- sim programs */
 #define GW_SIM_TEAM_BATTLE  1   /* examples/sim/team_battle_example.py:33-59 */
 #define GW_SIM_MAZE_NAV     2   /* examples/sim/maze_navigation.py:25-42     */
+#define GW_SIM_REACH_TARGET 3   /* examples/sim/reach_the_target.py:84-158   */
+
+/* attack actor of the sim */
+#define GW_ATTACK_BINARY     0  /* BinaryAttackActor     actor.py:441-501: one int, 0..simultaneous */
+#define GW_ATTACK_SELECTIVE  1  /* SelectiveAttackActor  actor.py:659-728: (2R+1)^2 ints, attacks per cell */
 
 /* done components (bit set; get_done = AND, get_all_done = AND: smart.py:106-117) */
 #define GW_DONE_ACTIVE        0x1u /* ActiveDone            done.py:39-56   */
@@ -141,7 +151,23 @@ typedef struct gw_config {
     int32_t  target_agent;         /* MazeNav: index of 'target' (else -1)      */
     int32_t  nav_agent;            /* MazeNav: index of 'navigator' (else -1)   */
     const gw_agent_spec* agents;   /* host pointer, n_agents entries            */
+    int32_t  attack_kind;          /* GW_ATTACK_*                               */
 } gw_config;
+
+/* Width of one entity's action: {move_row, move_col, attack...}.  The attack
+   part is one int (binary) or per-cell attack counts (selective): room for
+   (2R+1)^2 ints, R = the largest attack range; an agent of range r uses the
+   first (2r+1)^2 of them as its row-major window.  A negative first attack
+   int marks an entity that is not in the action dict.                       */
+static inline int32_t gw_config_act_dim(const gw_config* cfg)
+{
+    if (cfg->attack_kind != GW_ATTACK_SELECTIVE) return GW_ACT_DIM;
+    int32_t r = 0;
+    for (int32_t a = 0; a < cfg->n_agents; a++)
+        if ((cfg->agents[a].kind & GW_K_ATTACKING) && cfg->agents[a].attack_range > r)
+            r = cfg->agents[a].attack_range;
+    return 2 + (2 * r + 1) * (2 * r + 1);
+}
 
 typedef struct gw_engine* gw_handle;
 
@@ -166,14 +192,17 @@ gw_status gw_reset(gw_handle h, const uint8_t* mask, const uint8_t* all_done,
                    int32_t horizon, int32_t* obs, uint32_t* err_flags, void* stream);
 
 /* One AllStepManager.step for every env.
-     actions   device int32[E][A][GW_ACT_DIM]  (ignored for done entities)
+     actions   device int32[E][A][gw_act_dim(h)]  (ignored for done entities)
      obs       device int32[E][A][S][S]  (-2 for entities that are done)
      reward    device double[E][A]      (0 for entities that are done)
      done      device uint8[E][A]       (1 for entities that were already done)
      all_done  device uint8[E]          ('__all__')
-     acting    device uint64[E] or NULL (+= number of acting agents, for metrics) */
+     acting    device uint64[E] or NULL (+= number of acting agents, for metrics)
+     err_flags device uint32[E] or NULL (|= GW_ERR_*: a step the reference
+               would raise in; that env's outputs are not written)          */
 gw_status gw_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
-                  uint8_t* done, uint8_t* all_done, uint64_t* acting, void* stream);
+                  uint8_t* done, uint8_t* all_done, uint64_t* acting, uint32_t* err_flags,
+                  void* stream);
 
 /* gw_step followed, in the same launch, by AllStepManager.reset of every env
    whose '__all__' is set or that reached `horizon` steps (horizon > 0).  For
@@ -222,6 +251,7 @@ gw_status gw_destroy(gw_handle h);
 int32_t     gw_num_envs(gw_handle h);
 int32_t     gw_obs_side(gw_handle h);
 int32_t     gw_num_lanes(gw_handle h);
+int32_t     gw_act_dim(gw_handle h);
 /* entity index (into gw_config.agents) of each lane; out: host int32[A]     */
 gw_status   gw_lane_entities(gw_handle h, int32_t* out);
 const char* gw_last_error(void);

@@ -42,6 +42,7 @@ def lib():
         L.gwo_reset.argtypes = [vp, vp, vp, C.c_int32, vp, vp]
         L.gwo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.gwo_step_masked.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+        L.gwo_get_err.argtypes = [vp, vp]
         L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
         L.gwo_mt_probe.argtypes = [C.c_uint32, C.c_int32, C.c_uint32, C.c_int32, vp]
@@ -89,6 +90,11 @@ class Oracle:
         mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         self.L.gwo_step_masked(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
                                _p(acting), _p(mask))
+
+    def errors(self):
+        out = np.zeros(self.E, np.uint32)
+        self.L.gwo_get_err(self.h, _p(out))
+        return out
 
     def state(self):
         E, A = self.E, self.A

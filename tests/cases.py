@@ -4,13 +4,14 @@ import os
 
 import numpy as np
 
-from abmarl_amd.examples import TeamBattleSim, MazeNavigationAgent, MazeNavigationSim
+from abmarl_amd.examples import (TeamBattleSim, MazeNavigationAgent, MazeNavigationSim,
+                                 ReachTheTargetSim, RunningAgent, TargetAgent, BarrierAgent)
 from abmarl_amd.sim.gridworld.agent import (
     GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
-                'maze_file', 'maze_16']
+                'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -37,10 +38,30 @@ def build_maze(c):
         states={'PositionState'}, observers={'PositionCenteredEncodingObserver'})
 
 
+def build_rtt(c):
+    """ReachTheTarget as in the reference's examples/rllib_reach_the_target.py."""
+    R, C = c['rows'], c['cols']
+    corners = [[0, 0], [R - 1, 0], [0, C - 1], [R - 1, C - 1]]
+    agents = {f'barrier{i}': BarrierAgent(id=f'barrier{i}') for i in range(c['n_barriers'])}
+    for i in range(c['n_runners']):
+        kw = dict(c['runner'])
+        if c.get('corners'):
+            kw['initial_position'] = np.array(corners[i % 4], dtype=int)
+        agents[f'runner{i}'] = RunningAgent(id=f'runner{i}', **kw)
+    kw = dict(c['target'])
+    if c.get('corners'):
+        kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
+    agents['target'] = TargetAgent(**kw)
+    return ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
+                                       attack_mapping={2: {3}})
+
+
 def build_sim(c):
     """The golden case's configuration, built with the host API."""
     if c.get('kind') == 'maze':
         return build_maze(c)
+    if c.get('kind') == 'rtt':
+        return build_rtt(c)
     agents = {}
     for i in range(c['n_agents']):
         kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])

@@ -63,6 +63,24 @@ CASES = [
     # (examples/rllib_maze_navigation.py: view 2, walls blocking)
     dict(name='maze_file', kind='maze', maze='maze.txt', n_envs=4, n_steps=150, horizon=100,
          seed_base=3, agent=dict(move_range=1, view_range=2)),
+    # ReachTheTarget (examples/rllib_reach_the_target.py layout: 10 barriers,
+    # runners in the corners, the target in the center; view ranges equal)
+    dict(name='rtt_7', kind='rtt', rows=7, cols=7, n_barriers=10, n_runners=4, n_envs=4,
+         n_steps=120, horizon=40, seed_base=21, corners=True,
+         runner=dict(move_range=2, view_range=3, initial_health=1),
+         target=dict(view_range=3, attack_range=1, attack_strength=1, attack_accuracy=1)),
+    # larger, random placement and health, partial accuracy, 2 attacks per cell
+    dict(name='rtt_16', kind='rtt', rows=16, cols=16, n_barriers=30, n_runners=20, n_envs=3,
+         n_steps=100, horizon=60, seed_base=33,
+         runner=dict(move_range=2, view_range=3),
+         target=dict(view_range=3, attack_range=2, attack_strength=0.6, attack_accuracy=0.8,
+                     simultaneous_attacks=2)),
+    # crowded: runners placed on the target's cell get killed there by its
+    # center attack, then removed again in the move pass -> KeyError (recorded)
+    dict(name='rtt_double', kind='rtt', rows=5, cols=5, n_barriers=3, n_runners=14, n_envs=6,
+         n_steps=80, horizon=25, seed_base=44,
+         runner=dict(move_range=1, view_range=2, initial_health=1),
+         target=dict(view_range=2, attack_range=1, attack_strength=1, attack_accuracy=1)),
     # MazeNavigation 16x16 from generate_maze (utils.py:120-212), N and T on passages
     dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
          horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
@@ -94,6 +112,11 @@ def maze_array(spec):
 
 def full_case(case):
     c = dict(case)
+    if c.get('kind') == 'rtt':
+        c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
+        c['action_seed'] = 1234 + c['seed_base']
+        c['agent'] = dict(view_range=c['runner']['view_range'])
+        return c
     if c.get('kind') == 'maze':
         c['maze'] = maze_array(c['maze'])
         c.setdefault('state_order', 'position_health')
@@ -125,9 +148,19 @@ def full_case(case):
     return c
 
 
-def make_actions(c, A):
+def make_actions(c, A, managers=None):
     rng = np.random.RandomState(c['action_seed'])
     T, E = c['n_steps'], c['n_envs']
+    if c.get('kind') == 'rtt':
+        # [move_row, move_col, attack cells ((2R+1)^2, row-major)]
+        ra = c['target']['attack_range']
+        simul = c['target'].get('simultaneous_attacks', 1)
+        D = 2 * ra + 1
+        act = np.zeros((T, E, A, 2 + D * D), dtype=np.int8)
+        mr = c['runner']['move_range']
+        act[..., 0:2] = rng.randint(-mr, mr + 1, size=(T, E, A, 2))
+        act[..., 2:] = rng.randint(0, simul + 1, size=(T, E, A, D * D))
+        return act
     mr = c['agent']['move_range']
     act = np.zeros((T, E, A, 3), dtype=np.int8)
     act[..., 0:2] = rng.randint(-mr, mr + 1, size=(T, E, A, 2))
@@ -151,9 +184,31 @@ def build_reference_maze(c):
     return AllStepManager(sim)
 
 
+def build_reference_rtt(c):
+    from abmarl.examples import ReachTheTargetSim, RunningAgent, TargetAgent, BarrierAgent
+    from abmarl.managers import AllStepManager
+    R, C = c['rows'], c['cols']
+    corners = [[0, 0], [R - 1, 0], [0, C - 1], [R - 1, C - 1]]
+    agents = {f'barrier{i}': BarrierAgent(id=f'barrier{i}') for i in range(c['n_barriers'])}
+    for i in range(c['n_runners']):
+        kw = dict(c['runner'])
+        if c.get('corners'):
+            kw['initial_position'] = np.array(corners[i % 4], dtype=int)
+        agents[f'runner{i}'] = RunningAgent(id=f'runner{i}', **kw)
+    kw = dict(c['target'])
+    if c.get('corners'):
+        kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
+    agents['target'] = TargetAgent(**kw)
+    sim = ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
+                                      attack_mapping={2: {3}})
+    return AllStepManager(sim)
+
+
 def build_reference_env(c):
     if c['kind'] == 'maze':
         return build_reference_maze(c)
+    if c['kind'] == 'rtt':
+        return build_reference_rtt(c)
     from abmarl.examples.sim.team_battle_example import TeamBattleSim
     from abmarl.sim.gridworld.agent import GridWorldAgent
     from abmarl.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent, \
@@ -208,6 +263,7 @@ def run_case(case):
     ids = list(managers[0].agents.keys())        # entities, agents-dict order
     A = len(ids)
     act = make_actions(c, A)
+    agents0 = list(managers[0].agents.values())
 
     def obs_array(obs_dict):
         out = np.full((A, S, S), -2, dtype=np.int8)
@@ -238,6 +294,7 @@ def run_case(case):
         mt_pos=np.zeros((T, E), dtype=np.int16),
         mt_crc=np.zeros((T, E), dtype=np.uint32),
         reset_mask=np.zeros((T, E), dtype=np.uint8),
+        err=np.zeros((T, E), dtype=np.uint8),
         reset_obs=np.full((T, E, A, S, S), -2, dtype=np.int8),
     )
     steps = [0] * E
@@ -248,8 +305,34 @@ def run_case(case):
             adict = {}
             for i, aid in enumerate(ids):
                 if aid not in m.done_agents:
-                    adict[aid] = {'move': act[t, e, i, :2].astype(int), 'attack': int(act[t, e, i, 2])}
-            o, r, d, _ = m.step(adict)
+                    if c['kind'] == 'rtt':
+                        a = {}
+                        ag = agents0[i]
+                        if hasattr(ag, 'move_range'):
+                            a['move'] = act[t, e, i, :2].astype(int)
+                        if hasattr(ag, 'attack_range'):
+                            d = 2 * ag.attack_range + 1
+                            a['attack'] = act[t, e, i, 2:2 + d * d].astype(int).reshape(d, d)
+                        adict[aid] = a
+                    else:
+                        adict[aid] = {'move': act[t, e, i, :2].astype(int),
+                                      'attack': int(act[t, e, i, 2])}
+            try:
+                o, r, d, _ = m.step(adict)
+            except KeyError:
+                # reach_the_target.py:118-120, Grid.remove of a runner the
+                # target already killed on its cell: the env must be reset
+                out['err'][t, e] = 1
+                steps[e] = c['horizon']
+                out['mt_pos'][t, e] = np.random.get_state()[2]
+                out['mt_crc'][t, e] = zlib.crc32(np.ascontiguousarray(np.random.get_state()[1],
+                                                                      dtype=np.uint32).tobytes())
+                ro = m.reset()
+                steps[e] = 0
+                out['reset_mask'][t, e] = 1
+                out['reset_obs'][t, e], _ = obs_array(ro)
+                rng_states[e] = np.random.get_state()
+                continue
             steps[e] += 1
             out['obs'][t, e], out['returned'][t, e] = obs_array(o)
             for i, aid in enumerate(ids):

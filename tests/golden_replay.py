@@ -8,8 +8,25 @@ def _bits(x):
     return np.ascontiguousarray(x, dtype=np.float64).view(np.uint64)
 
 
-def check_step(g, t, obs, rew, done, all_done, state=None, where=''):
+def check_step(g, t, obs, rew, done, all_done, state=None, where='', errors=None):
+    """Compare one step.  Envs whose reference step raised (fixture 'err':
+    ReachTheTarget's double remove) have no reference outputs: for them only
+    the error flag and the RNG state are checked."""
     E = g['all_done'].shape[1]
+    err = g['err'][t].astype(bool) if 'err' in g else np.zeros(E, bool)
+    if err.any():
+        assert errors is not None, f"{where} step {t}: runner reports no errors"
+        assert ((errors[err] & 4) != 0).all(), f"{where} step {t}: KeyError flag missing"
+        assert ((errors[~err] & 4) == 0).all(), f"{where} step {t}: spurious KeyError flag"
+        g = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in g.items()}
+        g['obs'][t][err] = obs[err]
+        g['reward'][t][err] = rew[err]
+        g['done'][t][err] = done[err]
+        g['all_done'][t][err] = all_done[err]
+        if state is not None:
+            g['pos'][t][err] = state['pos'][err]
+            g['health'][t][err] = state['health'][err]
+            g['active'][t][err] = ((state['flags'] >> 2) & 1)[err]
     ok_obs = obs.astype(np.int64) == g['obs'][t].astype(np.int64)
     assert ok_obs.all(), f"{where} step {t}: obs mismatch at {np.argwhere(~ok_obs)[:5].tolist()}"
     bad = _bits(rew) != _bits(g['reward'][t])
@@ -39,7 +56,8 @@ def replay(runner, g, with_state=True, steps=None):
     for t in range(T):
         obs, rew, done, all_done = runner.step(g['actions'][t].astype(np.int32))
         st = runner.state() if with_state else None
-        check_step(g, t, obs, rew, done, all_done, st, where=type(runner).__name__)
+        errs = runner.errors() if hasattr(runner, 'errors') else None
+        check_step(g, t, obs, rew, done, all_done, st, where=type(runner).__name__, errors=errs)
         m = g['reset_mask'][t].astype(np.uint8)
         if m.any():
             robs = runner.reset(m)

@@ -13,9 +13,12 @@ HEADER = os.path.join(ROOT, 'include', 'gw_engine.h')
 
 
 def header_functions():
+    """Exported entry points (header-only `static inline` helpers excluded)."""
     txt = open(HEADER).read()
     txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
-    return sorted(set(re.findall(r'\b(gw_[a-z_]+)\s*\(', txt)))
+    inline = set(re.findall(r'static\s+inline\s+\w+\s+(gw_[a-z_]+)\s*\(', txt))
+    txt = re.sub(r'static\s+inline[^{]*\{.*?\n\}', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(gw_[a-z_]+)\s*\(', txt)) - inline)
 
 
 def header_defines():

@@ -22,8 +22,19 @@ def _check_obs(d, ref, returned, index):
         np.testing.assert_array_equal(d[k]['position_centered_encoding'], ref[index[k]])
 
 
+def _action(agent, a):
+    """The reference harness's action dict for one agent (make_golden.py)."""
+    out = {}
+    if hasattr(agent, 'move_range'):
+        out['move'] = a[:2].astype(int)
+    if hasattr(agent, 'attack_range'):
+        d = 2 * agent.attack_range + 1
+        out['attack'] = a[2:2 + d * d].astype(int).reshape(d, d) if a.size > 3 else int(a[2])
+    return out
+
+
 @pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners', 'tb_walls',
-                                  'maze_file', 'maze_16'])
+                                  'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double'])
 def test_dict_api_matches_reference(name):
     g = load_golden(name)
     c = g['case']
@@ -38,9 +49,17 @@ def test_dict_api_matches_reference(name):
         _check_obs(obs, g['obs0'][e], agents0, index)
         for t in range(g['actions'].shape[0]):
             done_agents = env.sim.done_agents
-            adict = {k: {'move': g['actions'][t, e, i, :2].astype(int),
-                         'attack': int(g['actions'][t, e, i, 2])}
+            adict = {k: _action(sim.agents[k], g['actions'][t, e, i])
                      for i, k in enumerate(ids) if k not in done_agents}
+            if 'err' in g and g['err'][t, e]:
+                with pytest.raises(KeyError):            # reach_the_target.py:118-120
+                    env.step(adict)
+                st = np.random.get_state()
+                assert st[2] == g['mt_pos'][t, e]
+                assert zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes()) == g['mt_crc'][t, e]
+                ro = env.reset()
+                _check_obs(ro, g['reset_obs'][t, e], agents0, index)
+                continue
             o, r, d, _ = env.step(adict)
             _check_obs(o, g['obs'][t, e], g['returned'][t, e], index)
             for k, v in r.items():

@@ -31,6 +31,9 @@ class OracleRunner:
     def state(self):
         return self.o.state()
 
+    def errors(self):
+        return self.o.errors()
+
 
 @pytest.mark.parametrize('name', GOLDEN_CASES)
 def test_oracle_matches_reference(oracle_mod, name):
