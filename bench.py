@@ -108,6 +108,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--autoreset', choices=['next_step', 'same_step'], default='next_step')
+    ap.add_argument('--no-other', action='store_true', help='skip the other auto-reset mode')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -177,7 +178,7 @@ def main():
     A, S = eng.A, cc.obs_side
     stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
     del eng
-    _, r2 = run(other)
+    r2 = None if args.no_other else run(other)[1]
     acting_all, dt_all, envs_all, step_ms = r['acting'], r['dt'], r['envs'], r['step_ms']
     step_ms_all = r['step_ms_max']
 
@@ -215,9 +216,10 @@ def main():
                          'bytes_per_launch': nbytes},
             'episode_stats': stats,
             'autoreset': args.autoreset,
-            'other_autoreset': {'mode': other, 'value': round(r2['acting'] / r2['dt'], 1),
-                                'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
-                                'kernel_ms': round(r2['step_ms_max'], 4)},
+            'other_autoreset': None if r2 is None else {
+                'mode': other, 'value': round(r2['acting'] / r2['dt'], 1),
+                'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
+                'kernel_ms': round(r2['step_ms_max'], 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds, horizon=args.horizon,

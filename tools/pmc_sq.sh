@@ -7,7 +7,7 @@ TAG=${1:-sq}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 bench.py --no-cpu-baseline --steps 30 --warmup 5"
+CMD="python3 bench.py --no-cpu-baseline --no-other --steps 30 --warmup 5"
 i=0
 for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

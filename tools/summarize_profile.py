@@ -60,7 +60,7 @@ def main():
                 pmc[counter] = sum(v) / len(v)
     lines = [f"# rocprofv3 summary `{tag}`", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
-             "--no-cpu-baseline --steps 200 --warmup 20` (PMC passes: `--pmc FETCH_SIZE` and "
+             "--no-cpu-baseline --no-other --steps 200 --warmup 20` (next_step auto-reset; PMC passes: `--pmc FETCH_SIZE` and "
              "`--pmc WRITE_SIZE`, separate runs, `--steps 30 --warmup 5`).", "",
              "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
     for r in rows[:8]:
