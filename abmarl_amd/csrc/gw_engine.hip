@@ -1924,24 +1924,34 @@ __device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
     return ctr;
 }
 
-__global__ void random_actions_kernel(const DevAgent* spec, int E, int A, uint64_t key,
+// the policy's per-agent constants, packed into the kernel arguments (no
+// dependent global load before the first store): kind | move_range << 8 |
+// attack_range << 16 | simultaneous << 20
+struct PolicySpec { uint32_t w[GW_MAX_AGENTS]; };
+
+__global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
                                       uint32_t step, uint32_t env_offset, int32_t* actions,
                                       int act_dim, int attack_kind)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= E * A) return;
-    const int e = i / A, a = i % A;
-    const DevAgent s = spec[a];
+    // one wave per env, one lane per agent (no index division); 16 envs per
+    // workgroup keep the dispatch count at ~one workgroup per CU
+    const int e = blockIdx.x * 16 + (int)(threadIdx.x >> 6), a = threadIdx.x & 63;
+    if (e >= E || a >= A) return;
+    const size_t i = (size_t)e * A + a;
+    const uint32_t pw = ps.w[a];
+    struct { uint32_t kind; int move_range, attack_range, simul; } s =
+        {pw & 0xffu, (int)((pw >> 8) & 0xffu), (int)((pw >> 16) & 0xfu), (int)(pw >> 20)};
     const uint2 k2 = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     uint4 r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED), k2);
     const int m = s.move_range;
     const uint32_t span = (uint32_t)(2 * m + 1);
     int32_t* o = actions + (size_t)i * act_dim;
-    o[0] = (s.kind & GW_K_MOVING) ? (int32_t)(r.x % span) - m : 0;
-    o[1] = (s.kind & GW_K_MOVING) ? (int32_t)(r.y % span) - m : 0;
+    // uniform on [0, n) by multiply-high (no integer division)
+    o[0] = (s.kind & GW_K_MOVING) ? (int32_t)__umulhi(r.x, span) - m : 0;
+    o[1] = (s.kind & GW_K_MOVING) ? (int32_t)__umulhi(r.y, span) - m : 0;
     const uint32_t na = (uint32_t)(s.simul + 1);
     if (attack_kind != GW_ATTACK_SELECTIVE) {
-        o[2] = (s.kind & GW_K_ATTACKING) ? (int32_t)(r.z % na) : 0;
+        o[2] = (s.kind & GW_K_ATTACKING) ? (int32_t)__umulhi(r.z, na) : 0;
         return;
     }
     // SelectiveAttackActor: Box(0, simultaneous, (2r+1, 2r+1)) per cell
@@ -1951,7 +1961,7 @@ __global__ void random_actions_kernel(const DevAgent* spec, int E, int A, uint64
         if ((q & 3) == 0 && q > 0)
             r = philox(make_uint4((uint32_t)e + env_offset, step, (uint32_t)a, 0x5EED + (uint32_t)(q >> 2)), k2);
         const uint32_t w = (q & 3) == 0 ? r.z : (q & 3) == 1 ? r.w : (q & 3) == 2 ? r.x : r.y;
-        o[2 + q] = q < nc ? (int32_t)(w % na) : 0;
+        o[2 + q] = q < nc ? (int32_t)__umulhi(w, na) : 0;
     }
 }
 
@@ -1969,6 +1979,7 @@ struct gw_engine {
     uint32_t* d_shadow;
     uint32_t* d_smask;
     int32_t lane_ent[GW_MAX_AGENTS];
+    PolicySpec policy;
     size_t smem_step, smem_reset;
 };
 
@@ -2214,6 +2225,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].attack_range = s.attack_range; hs[l].simul = s.simultaneous_attacks;
         hs[l].strength = s.attack_strength; hs[l].accuracy = s.attack_accuracy;
         hs[l].init_health = s.initial_health;
+    }
+    for (int l = 0; l < GW_MAX_AGENTS; l++) {
+        g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
+                                  ((uint32_t)(hs[l].attack_range & 0xf) << 16) |
+                                  ((uint32_t)(hs[l].simul & 0xfff) << 20)) : 0u;
     }
     HIPCHK(hipMalloc(&g->d_spec, sizeof(DevAgent) * A));
     HIPCHK(hipMemcpy(g->d_spec, hs, sizeof(DevAgent) * A, hipMemcpyHostToDevice));
@@ -2471,9 +2487,8 @@ gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t e
                             int32_t* actions, void* stream)
 {
     if (!g || !actions) return GW_E_INVALID;
-    const int n = g->E * g->A;
-    hipLaunchKernelGGL(random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                       (hipStream_t)stream, g->d_spec, g->E, g->A, key, step, env_offset, actions,
+    hipLaunchKernelGGL(random_actions_kernel, dim3((g->E + 15) / 16), dim3(16 * WAVE), 0,
+                       (hipStream_t)stream, g->policy, g->E, g->A, key, step, env_offset, actions,
                        g->base.act_dim, g->base.attack_kind);
     HIPCHK(hipGetLastError());
     return GW_OK;
