@@ -29,8 +29,16 @@ class Box(Space):
     def __init__(self, low, high, shape=None, dtype=np.float32):
         shape = tuple(shape) if shape is not None else np.shape(low)
         super().__init__(shape, dtype)
-        self.low = np.broadcast_to(np.asarray(low, dtype=self.dtype), shape).copy()
-        self.high = np.broadcast_to(np.asarray(high, dtype=self.dtype), shape).copy()
+        lo = np.broadcast_to(np.asarray(low, dtype=np.float64), shape)
+        hi = np.broadcast_to(np.asarray(high, dtype=np.float64), shape)
+        # boundedness is judged before the cast (an int Box cannot hold inf)
+        self.bounded_below = np.isfinite(lo)
+        self.bounded_above = np.isfinite(hi)
+        with np.errstate(invalid='ignore'):
+            self.low = np.where(self.bounded_below, lo, 0).astype(self.dtype) \
+                if np.issubdtype(self.dtype, np.integer) else lo.astype(self.dtype)
+            self.high = np.where(self.bounded_above, hi, 0).astype(self.dtype) \
+                if np.issubdtype(self.dtype, np.integer) else hi.astype(self.dtype)
 
     def contains(self, x):
         if type(x) is int:
@@ -74,6 +82,27 @@ class Discrete(Space):
 
     def __repr__(self):
         return f"Discrete({self.n})"
+
+
+class MultiDiscrete(Space):
+    """Vector of discrete values, element i in [0, nvec[i])."""
+
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec, dtype=np.int64)
+        super().__init__(self.nvec.shape, np.int64)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.nvec.shape and bool(np.all((0 <= x) & (x < self.nvec)))
+
+    def sample(self):
+        return (self._rng.random_sample(self.nvec.shape) * self.nvec).astype(np.int64)
+
+    def __eq__(self, other):
+        return isinstance(other, MultiDiscrete) and np.array_equal(self.nvec, other.nvec)
+
+    def __repr__(self):
+        return f"MultiDiscrete({self.nvec.tolist()})"
 
 
 class MultiBinary(Space):
