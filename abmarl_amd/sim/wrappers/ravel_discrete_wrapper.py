@@ -13,7 +13,7 @@ convention (abmarl_amd/external/rllib_multiagentenv_wrapper.py).
 """
 import numpy as np
 
-from abmarl_amd.spaces import Box, Discrete, MultiDiscrete, MultiBinary, Dict
+from abmarl_amd.spaces import Box, Discrete, MultiDiscrete, MultiBinary, Dict, Tuple
 from abmarl_amd.sim.agent_based_simulation import Agent
 from abmarl_amd.sim.wrappers.sar_wrapper import SARWrapper
 
@@ -31,7 +31,7 @@ def _parts(space):
                 for lo, h in zip(space.low.reshape(-1), space.high.reshape(-1))]
     if isinstance(space, Dict):
         return [(cardinality(s), s) for s in space.spaces.values()]
-    if isinstance(space, (tuple, list)):
+    if isinstance(space, (Tuple, tuple, list)):
         return [(cardinality(s), s) for s in space]
     raise TypeError(f"{space} cannot be ravelled")
 
@@ -96,7 +96,7 @@ def check_space(space):
             and bool(np.all(space.bounded_above))
     if isinstance(space, Dict):
         return all(check_space(s) for s in space.spaces.values())
-    if isinstance(space, (tuple, list)):
+    if isinstance(space, (Tuple, tuple, list)):
         return all(check_space(s) for s in space)
     return False
 

@@ -57,7 +57,7 @@ class Box(Space):
 
     def __eq__(self, other):
         return isinstance(other, Box) and self.shape == other.shape and \
-            np.array_equal(self.low, other.low) and np.array_equal(self.high, other.high)
+            np.allclose(self.low, other.low) and np.allclose(self.high, other.high)
 
     def __repr__(self):
         return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
@@ -163,14 +163,55 @@ class Dict(Space):
         return "Dict(" + ", ".join(f"{k}: {v}" for k, v in self.spaces.items()) + ")"
 
 
+class Tuple(Space):
+    """Ordered product of spaces (gym's Tuple)."""
+
+    def __init__(self, spaces):
+        self.spaces = tuple(spaces)
+        super().__init__(None, None)
+
+    def __getitem__(self, i):
+        return self.spaces[i]
+
+    def __len__(self):
+        return len(self.spaces)
+
+    def __iter__(self):
+        return iter(self.spaces)
+
+    def seed(self, seed=None):
+        for i, s in enumerate(self.spaces):
+            s.seed(None if seed is None else seed + i)
+        return [seed]
+
+    def contains(self, x):
+        if isinstance(x, list):
+            x = tuple(x)
+        return isinstance(x, tuple) and len(x) == len(self.spaces) and \
+            all(s.contains(p) for s, p in zip(self.spaces, x))
+
+    def sample(self):
+        return tuple(s.sample() for s in self.spaces)
+
+    def __eq__(self, other):
+        return isinstance(other, Tuple) and self.spaces == other.spaces
+
+    def __repr__(self):
+        return "Tuple(" + ", ".join(map(repr, self.spaces)) + ")"
+
+
 def check_space(space, strict=False):
     """abmarl/tools/gym_utils.py:27-51."""
-    if isinstance(space, (Box, Discrete, MultiBinary)):
+    if isinstance(space, (Box, Discrete, MultiDiscrete, MultiBinary)):
         return True
     if isinstance(space, Dict):
         return all(check_space(s) for s in space.spaces.values())
+    if isinstance(space, Tuple):
+        return all(check_space(s) for s in space.spaces)
     if not strict and isinstance(space, dict):
         return all(check_space(s) for s in space.values())
+    if not strict and isinstance(space, tuple):
+        return all(check_space(s) for s in space)
     return False
 
 
