@@ -1,0 +1,60 @@
+"""TurnBasedManager (reference: abmarl/managers/turn_based_manager.py:8-94).
+
+Agents act one at a time in agents-dict order.  reset returns the
+observation of the agent whose turn it is; step takes that agent's action
+and returns the outputs of the next agent in line, preceded by those of any
+agent that finished since its last turn (so each agent sees its own final
+obs/reward/done once).  Once the simulation reports all done, every agent
+not yet done gets its outputs.
+
+As in the reference, the turn order is one endless cycle built at
+construction: reset() does NOT restart it, so an episode begins with the
+agent after the one that ended the previous episode's loop.
+"""
+from itertools import cycle
+
+from abmarl_amd.sim.agent_based_simulation import Agent
+from abmarl_amd.managers.simulation_manager import SimulationManager
+
+
+class TurnBasedManager(SimulationManager):
+    def __init__(self, sim, **kwargs):
+        super().__init__(sim, **kwargs)
+        self.agent_order = cycle([aid for aid, a in self.agents.items() if isinstance(a, Agent)])
+
+    def reset(self, **kwargs):
+        self.done_agents = {aid for aid, a in self.agents.items() if not isinstance(a, Agent)}
+        self.sim.reset(**kwargs)
+        first = next(self.agent_order)
+        return {first: self.sim.get_obs(first)}
+
+    def _collect(self, aid, out):
+        obs, rewards, dones, infos = out
+        obs[aid] = self.sim.get_obs(aid)
+        rewards[aid] = self.sim.get_reward(aid)
+        dones[aid] = self.sim.get_done(aid)
+        infos[aid] = self.sim.get_info(aid)
+
+    def step(self, action_dict, **kwargs):
+        actor = next(iter(action_dict))
+        assert actor not in self.done_agents, \
+            "Received an action for an agent that is already done."
+        self.sim.step(action_dict, **kwargs)
+        out = ({}, {}, {'__all__': self.sim.get_all_done()}, {})
+        if out[2]['__all__']:
+            for aid in self.agents:
+                if aid not in self.done_agents:
+                    self._collect(aid, out)
+            return out
+        for aid in self.agent_order:
+            if aid in self.done_agents:
+                continue
+            self._collect(aid, out)
+            if not out[2][aid]:
+                break                          # the next agent to act
+            # finished since its last turn: report it once, keep looking
+            self.done_agents.add(aid)
+            if not (self.agents.keys() - self.done_agents):
+                out[2]['__all__'] = True
+                break
+        return out

@@ -388,12 +388,45 @@ def run_multicorridor(randomize=False, n_steps=60):
     print(f"{name}: {n_steps} steps -> {os.path.getsize(path)} B")
 
 
+def run_multicorridor_turn_based(n_steps=300):
+    """TurnBasedManager over MultiCorridor, np.random.seed(24)
+    (tests/test_turn_based_multi_corridor.py), scripted random actions for the
+    agent whose turn it is; the cycle is NOT restarted by reset (the
+    reference's agent_order is created once, turn_based_manager.py:17-20)."""
+    from abmarl.examples import MultiCorridor
+    from abmarl.managers import TurnBasedManager
+    rng = np.random.RandomState(7)
+    np.random.seed(24)
+    sim = TurnBasedManager(MultiCorridor())
+
+    def enc(d):
+        return {k: {kk: np.asarray(vv).tolist() for kk, vv in v.items()} for k, v in d.items()}
+
+    o = sim.reset()
+    records = [{'reset': enc(o)}]
+    for t in range(n_steps):
+        actor = [k for k in o if k not in sim.done_agents][-1]
+        acts = {actor: int(rng.choice(3, p=[0.2, 0.2, 0.6]))}   # mostly RIGHT
+        o, r, d, _ = sim.step(acts)
+        rec = {'actions': acts, 'obs': enc(o), 'reward': {k: float(v) for k, v in r.items()},
+               'done': {k: bool(v) for k, v in d.items()}}
+        if d['__all__']:
+            o = sim.reset()
+            rec['reset'] = enc(o)
+        records.append(rec)
+    path = os.path.join(HERE, 'multicorridor_turn.json')
+    json.dump(records, open(path, 'w'))
+    print(f"multicorridor_turn: {n_steps} steps -> {os.path.getsize(path)} B")
+
+
 def main():
     sys.path.insert(0, HERE)
     import gym_stub
     gym_stub.install()
     sys.path.insert(0, REF)
     only = sys.argv[1:]
+    if 'multicorridor_turn' in only:
+        run_multicorridor_turn_based()
     for case in CASES:
         if not only or case['name'] in only:
             run_case(case)
@@ -401,6 +434,7 @@ def main():
         return
     run_multicorridor(False)
     run_multicorridor(True)
+    run_multicorridor_turn_based()
 
 
 if __name__ == '__main__':
