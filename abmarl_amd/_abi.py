@@ -22,6 +22,7 @@ GW_E_UNSUPPORTED = -3
 GW_ERR_NO_CELL = 1
 GW_ERR_INIT_POSITION = 2
 GW_ERR_DOUBLE_REMOVE = 4
+GW_ERR_TUNNEL_PLACE = 8
 
 GW_K_OBSERVING = 0x01
 GW_K_ACTING = 0x02
@@ -31,10 +32,16 @@ GW_K_ATTACKING = 0x10
 GW_K_HEALTH = 0x20
 GW_K_PROGRAM = 0x80
 GW_K_BLOCKING = 0x40
+GW_K_ORIENTATION = 0x100
+GW_K_FOOD = 0x200
 
 GW_SIM_TEAM_BATTLE = 1
 GW_SIM_MAZE_NAV = 2
 GW_SIM_REACH_TARGET = 3
+GW_SIM_PACMAN = 4
+
+GW_OBS_POSITION_CENTERED = 0
+GW_OBS_ABSOLUTE = 1
 
 GW_ATTACK_BINARY = 0
 GW_ATTACK_SELECTIVE = 1
@@ -64,6 +71,7 @@ class AgentSpec(C.Structure):
         ("attack_strength", C.c_double),
         ("attack_accuracy", C.c_double),
         ("initial_health", C.c_double),
+        ("initial_orientation", C.c_int32),
     ]
 
 
@@ -85,6 +93,10 @@ class Config(C.Structure):
         ("nav_agent", C.c_int32),
         ("agents", C.POINTER(AgentSpec)),
         ("attack_kind", C.c_int32),
+        ("obs_kind", C.c_int32),
+        ("pacman_agent", C.c_int32),
+        ("tunnel", C.c_int32 * 4),
+        ("pac_rewards", C.c_double * 5),
     ]
 
 
@@ -94,7 +106,9 @@ class CompiledConfig:
     def __init__(self, rows, cols, specs, sim_kind, overlap, attack_mapping,
                  stacked_attacks=False, observe_self=True, no_overlap_at_reset=False,
                  state_order=GW_ORDER_POSITION_HEALTH, done_kind=GW_DONE_ACTIVE,
-                 obs_range=0, target_agent=-1, nav_agent=-1, attack_kind=0):
+                 obs_range=0, target_agent=-1, nav_agent=-1, attack_kind=0,
+                 obs_kind=GW_OBS_POSITION_CENTERED, pacman_agent=-1, tunnel=(-1, -1, -1, -1),
+                 pac_rewards=(0.0, 0.0, 0.0, 0.0, 0.0)):
         self.n_agents = len(specs)
         self._specs = (AgentSpec * max(1, self.n_agents))()
         for i, s in enumerate(specs):
@@ -114,9 +128,18 @@ class CompiledConfig:
         cfg.nav_agent = nav_agent
         cfg.agents = C.cast(self._specs, C.POINTER(AgentSpec))
         cfg.attack_kind = attack_kind
+        cfg.obs_kind = obs_kind
+        cfg.pacman_agent = pacman_agent
+        for i in range(4):
+            cfg.tunnel[i] = int(tunnel[i])
+        for i in range(5):
+            cfg.pac_rewards[i] = float(pac_rewards[i])
         self.cfg = cfg
         self.rows, self.cols = rows, cols
+        self.obs_kind = obs_kind
         self.obs_side = 2 * obs_range + 1
+        # per-entity observation shape (gw_obs_shape)
+        self.obs_shape = (rows, cols) if obs_kind == GW_OBS_ABSOLUTE else (self.obs_side,) * 2
         self.specs = list(specs)
         self.attack_kind = attack_kind
 

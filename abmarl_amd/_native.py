@@ -44,6 +44,15 @@ SIGNATURES = {
     'gw_num_lanes': (_i32, [_vp]),
     'gw_act_dim': (_i32, [_vp]),
     'gw_lane_entities': (_i32, [_vp, _vp]),
+    'gw_obs_shape': (_i32, [_vp, _vp, _vp]),
+    'gw_num_passive': (_i32, [_vp]),
+    'gw_turn_reset': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_turn_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    'gw_sim_reset': (_i32, [_vp, _vp, _vp, _vp]),
+    'gw_sim_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'gw_observe': (_i32, [_vp, _i32, _vp, _vp]),
+    'gw_get_aux_state': (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    'gw_set_aux_state': (_i32, [_vp, _vp, _vp, _vp, _vp]),
     'gw_last_error': (C.c_char_p, []),
     'gw_abi_version': (_i32, []),
 }
@@ -52,7 +61,7 @@ SIGNATURES = {
 def build(force=False, verbose=False, stamps=False, checks=False):
     """Compile the engine for gfx950 with hipcc (works without a GPU)."""
     out = LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB)
-    deps = [SRC, INCLUDE]
+    deps = [SRC, INCLUDE, os.path.join(os.path.dirname(SRC), 'gw_pacman.inc')]
     if not force and os.path.exists(out) and \
             os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out

@@ -68,6 +68,7 @@ struct DevAgent {               // per-entity constants (spec table in HBM)
     int32_t init_r, init_c;
     int32_t view_range, move_range, attack_range, simul;
     double strength, accuracy, init_health;
+    int32_t init_orient;
 };
 
 struct Params {
@@ -108,6 +109,20 @@ struct Params {
     const uint32_t* smask;
     int32_t shadow_off[GW_MAX_RANGE + 1];
     int32_t smask_off[GW_MAX_RANGE + 1];
+    // Pacman program (GW_SIM_PACMAN, gw_pacman.inc)
+    int32_t obs_kind, pacman, mode, obs_lane;
+    int32_t tunnel[4];
+    double prw[5];                         // bad_move, entropy, eat_food, kill, die
+    int32_t n_passive, pwords;             // passive entities (food), bit words per env
+    const int16_t* passive_cell;           // [n_passive] cell
+    const int16_t* cell_passive;           // [HW] passive index, -1 = none
+    const int8_t* passive_enc;             // [n_passive]
+    uint32_t* pbits;                       // [E][pwords] passive present
+    double* racc;                          // [E][A] SmartGWS.rewards accumulators
+    int32_t* cyc;                          // [E] TurnBasedManager cycle position (lane)
+    uint8_t* returned;                     // [E][A] lanes in the returned dicts
+    int32_t* turn;                         // [E] lane whose action the next call takes
+    uint64_t agent_lanes;                  // lanes that are Agents (the turn cycle)
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -1928,6 +1943,7 @@ __device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
 // dependent global load before the first store): kind | move_range << 8 |
 // attack_range << 16 | simultaneous << 20
 struct PolicySpec { uint32_t w[GW_MAX_AGENTS]; };
+constexpr int RA_CROSS = 100;   // random_actions_kernel: cross moves (Pacman program)
 
 __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
                                       uint32_t step, uint32_t env_offset, int32_t* actions,
@@ -1946,6 +1962,13 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
     const int m = s.move_range;
     const uint32_t span = (uint32_t)(2 * m + 1);
     int32_t* o = actions + (size_t)i * act_dim;
+    if (attack_kind == RA_CROSS) {
+        // CrossMoveActor / DriftMoveActor: Discrete(5); slot 2 >= 0 = in the dict
+        o[0] = (s.kind & GW_K_MOVING) ? (int32_t)__umulhi(r.x, 5u) : 0;
+        o[1] = 0;
+        o[2] = 0;
+        return;
+    }
     // uniform on [0, n) by multiply-high (no integer division)
     o[0] = (s.kind & GW_K_MOVING) ? (int32_t)__umulhi(r.x, span) - m : 0;
     o[1] = (s.kind & GW_K_MOVING) ? (int32_t)__umulhi(r.y, span) - m : 0;
@@ -1965,6 +1988,8 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
     }
 }
 
+#include "gw_pacman.inc"
+
 }  // namespace
 
 // ====================================================================== C-ABI
@@ -1981,6 +2006,10 @@ struct gw_engine {
     int32_t lane_ent[GW_MAX_AGENTS];
     PolicySpec policy;
     size_t smem_step, smem_reset;
+    // Pacman program
+    bool pacman;
+    int16_t* d_passive;        // passive_cell [n_passive] | cell_passive [HW]
+    int8_t* d_passive_enc;
 };
 
 // create_grid_and_mask (utils.py:46-115): the window cells of range R that a
@@ -2068,13 +2097,21 @@ static hipError_t launch_reset(const gw_engine* g, const Params& p, hipStream_t 
     default: return hipErrorInvalidValue;            \
     }
 
-static hipError_t do_step(const gw_engine* g, const Params& p, hipStream_t st)
+static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st)
 {
+    hipLaunchKernelGGL(pac_kernel, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    return hipGetLastError();
+}
+
+static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
+{
+    if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
     DISPATCH_S(g->S, launch_step, g, p, st);
 }
 
-static hipError_t do_reset(const gw_engine* g, const Params& p, hipStream_t st)
+static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 {
+    if (g->pacman) { p.mode = PAC_RESET_ALL; return launch_pac(g, p, st); }
     DISPATCH_S(g->S, launch_reset, g, p, st);
 }
 
@@ -2095,7 +2132,7 @@ static hipError_t set_attrs(int S, size_t a, size_t b)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 2; }
+int32_t gw_abi_version(void) { return 3; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
@@ -2115,7 +2152,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         return GW_E_UNSUPPORTED;
     }
     if (cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_MAZE_NAV &&
-        cfg->sim_kind != GW_SIM_REACH_TARGET) {
+        cfg->sim_kind != GW_SIM_REACH_TARGET && cfg->sim_kind != GW_SIM_PACMAN) {
         set_err("unknown sim_kind %d", cfg->sim_kind);
         return GW_E_INVALID;
     }
@@ -2123,7 +2160,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
         if (s.encoding < 1 || s.encoding > GW_MAX_ENC) { set_err("agent %d encoding %d", a, s.encoding); return GW_E_UNSUPPORTED; }
-        if ((s.kind & GW_K_GRID_OBSERVER) && s.view_range != cfg->obs_range) {
+        if ((s.kind & GW_K_GRID_OBSERVER) && cfg->obs_kind != GW_OBS_ABSOLUTE && s.view_range != cfg->obs_range) {
             set_err("agent %d view_range %d != obs_range %d", a, s.view_range, cfg->obs_range);
             return GW_E_UNSUPPORTED;
         }
@@ -2136,6 +2173,30 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     const bool maze = cfg->sim_kind == GW_SIM_MAZE_NAV;
     const bool rtt = cfg->sim_kind == GW_SIM_REACH_TARGET;
+    const bool pac = cfg->sim_kind == GW_SIM_PACMAN;
+    if ((cfg->obs_kind == GW_OBS_ABSOLUTE) != pac) {
+        set_err("the AbsoluteEncodingObserver runs with the Pacman program (and only it)");
+        return GW_E_UNSUPPORTED;
+    }
+    if (pac) {
+        // the program places every entity at its initial position (no two in
+        // one cell), keeps the food passive and has no blocking (gw_pacman.inc)
+        if (cfg->pacman_agent < 0 || cfg->pacman_agent >= NE) { set_err("pacman needs pacman_agent"); return GW_E_INVALID; }
+        std::vector<uint8_t> used(HW, 0);
+        for (int a = 0; a < NE; a++) {
+            const gw_agent_spec& s = cfg->agents[a];
+            if (s.init_row < 0 || s.init_col < 0) { set_err("pacman program: entity %d has no initial position", a); return GW_E_UNSUPPORTED; }
+            const int cell = s.init_row * cfg->cols + s.init_col;
+            if (used[cell]) { set_err("pacman program: entities share initial cell %d", cell); return GW_E_UNSUPPORTED; }
+            used[cell] = 1;
+            if (s.kind & GW_K_BLOCKING) { set_err("pacman program: blocking entity %d", a); return GW_E_UNSUPPORTED; }
+            if ((s.kind & GW_K_FOOD) && ((s.kind & ~(GW_K_FOOD | GW_K_HEALTH)) || s.initial_health < 0)) {
+                set_err("pacman program: food %d must be a HealthAgent with an initial health only", a);
+                return GW_E_UNSUPPORTED;
+            }
+        }
+        if (cfg->agents[cfg->pacman_agent].kind & GW_K_FOOD) { set_err("pacman is food"); return GW_E_INVALID; }
+    }
     if (maze && (cfg->nav_agent < 0 || cfg->nav_agent >= NE || cfg->target_agent < 0 || cfg->target_agent >= NE)) {
         set_err("maze navigation needs nav_agent/target_agent");
         return GW_E_INVALID;
@@ -2163,9 +2224,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int e = 0; e <= GW_MAX_ENC; e++) { attacked |= cfg->attack_mapping[e]; overlapped |= cfg->overlap[e]; }
     const uint32_t dynamic_kinds = GW_K_OBSERVING | GW_K_ACTING | GW_K_GRID_OBSERVER | GW_K_MOVING |
                                    GW_K_ATTACKING | GW_K_HEALTH;
-    std::vector<int> lanes, statics;
+    std::vector<int> lanes, statics, passive;
     for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
+        if (pac && (s.kind & GW_K_FOOD)) { passive.push_back(a); continue; }
         const bool st = !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
                         cfg->overlap[s.encoding] == 0 && !((overlapped >> s.encoding) & 1u) &&
                         !((attacked >> s.encoding) & 1u) &&
@@ -2175,6 +2237,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     const int A = (int)lanes.size();
     if (A == 0 || A > GW_MAX_AGENTS) {
         set_err("%d dynamic entities outside 1..%d (one wavefront lane each)", A, GW_MAX_AGENTS);
+        return GW_E_UNSUPPORTED;
+    }
+    if ((int)passive.size() > 32 * PAC_MAX_PWORDS) {
+        set_err("%d food entities > %d", (int)passive.size(), 32 * PAC_MAX_PWORDS);
         return GW_E_UNSUPPORTED;
     }
     std::vector<uint8_t> is_static(HW, 0);
@@ -2201,7 +2267,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     gw_engine* g = new gw_engine();
     memset(&g->base, 0, sizeof(Params));
     g->device = device; g->E = n_envs; g->A = A; g->H = cfg->rows; g->W = cfg->cols;
-    g->S = 2 * cfg->obs_range + 1; g->max_enc = max_enc;
+    g->S = pac ? 1 : 2 * cfg->obs_range + 1; g->max_enc = max_enc;
+    g->pacman = pac;
     for (int i = 0; i < A; i++) g->lane_ent[i] = lanes[i];
     const size_t EA = (size_t)n_envs * A;
     Params& p = g->base;
@@ -2225,6 +2292,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].attack_range = s.attack_range; hs[l].simul = s.simultaneous_attacks;
         hs[l].strength = s.attack_strength; hs[l].accuracy = s.attack_accuracy;
         hs[l].init_health = s.initial_health;
+        hs[l].init_orient = s.initial_orientation;
     }
     for (int l = 0; l < GW_MAX_AGENTS; l++) {
         g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
@@ -2264,6 +2332,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             ht[i] = (row < 0 || row >= cfg->rows || col < 0 || col >= cfg->cols) ? CELL_OFF : 0;
         }
         for (int a : statics) {
+            const gw_agent_spec& s = cfg->agents[a];
+            ht[(size_t)(s.init_row + pad) * p.pitch + (s.init_col + pad)] = (uint8_t)s.encoding;
+        }
+        for (int a : passive) {                 // present unless eaten (gw_pacman.inc)
             const gw_agent_spec& s = cfg->agents[a];
             ht[(size_t)(s.init_row + pad) * p.pitch + (s.init_col + pad)] = (uint8_t)s.encoding;
         }
@@ -2341,8 +2413,49 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
     g->smem_step = smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
+    if (pac) {
+        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE;
+        const size_t wb = work_bytes(HW, A, g->S, max_enc);
+        if (pw > wb) g->smem_step += pw - wb;
+    }
     g->smem_reset = g->smem_step;
     if (g->smem_step > 160 * 1024) { set_err("LDS need %zu B > 160 KiB", g->smem_step); return GW_E_UNSUPPORTED; }
+    if (pac) {
+        p.obs_kind = cfg->obs_kind;
+        for (int l = 0; l < A; l++) if (lanes[l] == cfg->pacman_agent) p.pacman = l;
+        for (int i = 0; i < 4; i++) p.tunnel[i] = cfg->tunnel[i];
+        for (int i = 0; i < 5; i++) p.prw[i] = cfg->pac_rewards[i];
+        p.agent_lanes = 0;
+        for (int l = 0; l < A; l++)
+            if ((hs[l].kind & GW_K_OBSERVING) && (hs[l].kind & GW_K_ACTING)) p.agent_lanes |= 1ull << l;
+        p.n_passive = (int)passive.size();
+        p.pwords = (p.n_passive + 31) / 32;
+        std::vector<int16_t> pc(p.n_passive + HW, (int16_t)-1);
+        std::vector<int8_t> pe(p.n_passive > 0 ? p.n_passive : 1, 0);
+        for (int k = 0; k < p.n_passive; k++) {
+            const gw_agent_spec& s = cfg->agents[passive[k]];
+            const int cell = s.init_row * cfg->cols + s.init_col;
+            pc[k] = (int16_t)cell;
+            pc[p.n_passive + cell] = (int16_t)k;
+            pe[k] = (int8_t)s.encoding;
+        }
+        HIPCHK(hipMalloc(&g->d_passive, pc.size() * 2));
+        HIPCHK(hipMemcpy(g->d_passive, pc.data(), pc.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&g->d_passive_enc, pe.size()));
+        HIPCHK(hipMemcpy(g->d_passive_enc, pe.data(), pe.size(), hipMemcpyHostToDevice));
+        p.passive_cell = g->d_passive;
+        p.cell_passive = g->d_passive + p.n_passive;
+        p.passive_enc = g->d_passive_enc;
+        const size_t pwn = (size_t)n_envs * (p.pwords > 0 ? p.pwords : 1);
+        HIPCHK(hipMalloc(&p.pbits, pwn * 4));
+        HIPCHK(hipMemset(p.pbits, 0, pwn * 4));
+        HIPCHK(hipMalloc(&p.cyc, (size_t)n_envs * 4));
+        HIPCHK(hipMemset(p.cyc, 0xff, (size_t)n_envs * 4));      // -1: no turn yet
+        HIPCHK(hipFuncSetAttribute((const void*)pac_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)g->smem_step));
+    }
+    HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
+    HIPCHK(hipMemset(p.racc, 0, EA * sizeof(double)));
     HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
     *out = g;
     return GW_OK;
@@ -2355,6 +2468,8 @@ gw_status gw_destroy(gw_handle g)
     (void)hipFree(g->base.seq); (void)hipFree(g->base.mt); (void)hipFree(g->base.steps);
     (void)hipFree(g->d_spec); (void)hipFree(g->d_tmpl); (void)hipFree(g->d_free);
     (void)hipFree(g->d_static_bits); (void)hipFree(g->d_shadow); (void)hipFree(g->d_smask);
+    (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
+    (void)hipFree(g->d_passive); (void)hipFree(g->d_passive_enc);
     delete g;
     return GW_OK;
 }
@@ -2467,6 +2582,103 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     return GW_OK;
 }
 
+gw_status gw_obs_shape(gw_handle g, int32_t* rows, int32_t* cols)
+{
+    if (!g || !rows || !cols) return GW_E_INVALID;
+    if (g->base.obs_kind == GW_OBS_ABSOLUTE) { *rows = g->H; *cols = g->W; }
+    else { *rows = g->S; *cols = g->S; }
+    return GW_OK;
+}
+
+int32_t gw_num_passive(gw_handle g) { return g ? g->base.n_passive : 0; }
+
+gw_status gw_turn_reset(gw_handle g, const uint8_t* mask, int32_t* obs, uint8_t* returned,
+                        int32_t* turn, uint32_t* err_flags, void* stream)
+{
+    if (!g || !obs || !returned || !turn) return GW_E_INVALID;
+    if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.mask = mask; p.obs = obs; p.returned = returned; p.turn = turn; p.err = err_flags;
+    p.mode = PAC_RESET_TURN;
+    if (!mask) {                     // every env: a mask-less reset of all
+        p.prev_all_done = nullptr; p.horizon = 0;
+    }
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_turn_step(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
+                       uint8_t* done, uint8_t* all_done, uint8_t* returned, int32_t* turn,
+                       uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream)
+{
+    if (!g || !actions || !obs || !reward || !done || !all_done || !returned || !turn) return GW_E_INVALID;
+    if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.returned = returned; p.turn = turn; p.acting = acting; p.horizon = horizon; p.err = err_flags;
+    p.mode = PAC_STEP_TURN;
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_sim_reset(gw_handle g, const uint8_t* mask, uint32_t* err_flags, void* stream)
+{
+    if (!g) return GW_E_INVALID;
+    if (!g->pacman) { set_err("simulation-only protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.mask = mask; p.err = err_flags; p.mode = PAC_RESET_SIM;
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_sim_step(gw_handle g, const int32_t* actions, double* reward, uint8_t* done,
+                      uint8_t* all_done, uint32_t* err_flags, void* stream)
+{
+    if (!g || !actions || !reward || !done || !all_done) return GW_E_INVALID;
+    if (!g->pacman) { set_err("simulation-only protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.actions = actions; p.reward = reward; p.done = done; p.all_done = all_done; p.err = err_flags;
+    p.mode = PAC_STEP_SIM;
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_observe(gw_handle g, int32_t lane, int32_t* obs, void* stream)
+{
+    if (!g || !obs || lane < 0 || lane >= g->A) return GW_E_INVALID;
+    if (!g->pacman) { set_err("on-demand observation: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.obs = obs; p.obs_lane = lane; p.mode = PAC_OBSERVE;
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_get_aux_state(gw_handle g, double* racc, uint32_t* passive_bits, int32_t* turn_pos,
+                           void* stream)
+{
+    if (!g) return GW_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t EA = (size_t)g->E * g->A;
+    if (racc) HIPCHK(hipMemcpyAsync(racc, g->base.racc, EA * 8, hipMemcpyDeviceToDevice, st));
+    if (passive_bits && g->base.pwords)
+        HIPCHK(hipMemcpyAsync(passive_bits, g->base.pbits, (size_t)g->E * g->base.pwords * 4, hipMemcpyDeviceToDevice, st));
+    if (turn_pos && g->base.cyc) HIPCHK(hipMemcpyAsync(turn_pos, g->base.cyc, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
+gw_status gw_set_aux_state(gw_handle g, const double* racc, const uint32_t* passive_bits,
+                           const int32_t* turn_pos, void* stream)
+{
+    if (!g) return GW_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t EA = (size_t)g->E * g->A;
+    if (racc) HIPCHK(hipMemcpyAsync(g->base.racc, racc, EA * 8, hipMemcpyDeviceToDevice, st));
+    if (passive_bits && g->base.pwords)
+        HIPCHK(hipMemcpyAsync(g->base.pbits, passive_bits, (size_t)g->E * g->base.pwords * 4, hipMemcpyDeviceToDevice, st));
+    if (turn_pos && g->base.cyc) HIPCHK(hipMemcpyAsync(g->base.cyc, turn_pos, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    return GW_OK;
+}
+
 // diagnostic hook (not in the public header): violation record for -DGW_CHECKS builds
 gw_status gw_debug_set_checks(gw_handle g, uint32_t* dbg)
 {
@@ -2489,7 +2701,7 @@ gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t e
     if (!g || !actions) return GW_E_INVALID;
     hipLaunchKernelGGL(random_actions_kernel, dim3((g->E + 15) / 16), dim3(16 * WAVE), 0,
                        (hipStream_t)stream, g->policy, g->E, g->A, key, step, env_offset, actions,
-                       g->base.act_dim, g->base.attack_kind);
+                       g->base.act_dim, g->pacman ? RA_CROSS : g->base.attack_kind);
     HIPCHK(hipGetLastError());
     return GW_OK;
 }

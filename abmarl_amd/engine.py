@@ -50,8 +50,13 @@ class GridWorldEngine:
         _native.check(self.L.gw_lane_entities(h, ents), 'gw_lane_entities')
         self.lane_entities = np.array(ents[:], dtype=np.int64)
         dev = self.device
-        E, A, S = self.E, self.A, self.S
-        self.obs = torch.full((E, A, S, S), -2, dtype=torch.int32, device=dev)
+        E, A = self.E, self.A
+        rows, cols = C.c_int32(), C.c_int32()
+        _native.check(self.L.gw_obs_shape(h, C.byref(rows), C.byref(cols)), 'gw_obs_shape')
+        self.obs_shape = (rows.value, cols.value)   # per lane: (S, S) or (rows, cols) absolute
+        self.n_passive = int(self.L.gw_num_passive(h))
+        self.pacman = compiled.cfg.sim_kind == _abi.GW_SIM_PACMAN
+        self.obs = torch.full((E, A) + self.obs_shape, -2, dtype=torch.int32, device=dev)
         self.reward = torch.zeros((E, A), dtype=torch.float64, device=dev)
         self.done = torch.ones((E, A), dtype=torch.uint8, device=dev)
         self.all_done = torch.zeros((E,), dtype=torch.uint8, device=dev)
@@ -142,6 +147,75 @@ class GridWorldEngine:
                 'gw_step_autoreset_next')
         self._check_debug('gw_step_autoreset_next')
         return self.obs, self.reward, self.done, self.all_done
+
+    # ------------------------------------------------- Pacman program protocols
+    def _turn_bufs(self):
+        if not hasattr(self, 'returned'):
+            self.returned = torch.zeros((self.E, self.A), dtype=torch.uint8, device=self.device)
+            self.turn = torch.full((self.E,), -1, dtype=torch.int32, device=self.device)
+        return self.returned, self.turn
+
+    def turn_reset(self, mask=None):
+        """TurnBasedManager.reset of the selected envs (all by default):
+        returns (obs, returned, turn)."""
+        ret, turn = self._turn_bufs()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_turn_reset(self.h, _ptr(mask), _ptr(self.obs), _ptr(ret),
+                                               _ptr(turn), _ptr(self.err), _stream()),
+                          'gw_turn_reset')
+        return self.obs, ret, turn
+
+    def turn_step(self, actions=None, horizon=0):
+        """TurnBasedManager.step with next-step auto-reset: the lane turn[e]
+        acts; returns (obs, reward, done, all_done, returned, turn)."""
+        a = self.actions if actions is None else actions
+        assert a.dtype == torch.int32 and a.is_contiguous() and a.shape == self.actions.shape
+        ret, turn = self._turn_bufs()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_turn_step(
+                self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                _ptr(self.all_done), _ptr(ret), _ptr(turn), _ptr(self.acting), int(horizon),
+                _ptr(self.err), _stream()), 'gw_turn_step')
+        return self.obs, self.reward, self.done, self.all_done, ret, turn
+
+    def sim_reset(self, mask=None):
+        """SmartGWS.reset only (no observation drawn)."""
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_sim_reset(self.h, _ptr(mask), _ptr(self.err), _stream()),
+                          'gw_sim_reset')
+
+    def sim_step(self, actions):
+        """sim.step(action_dict): reward = accumulated (not consumed), done, all_done."""
+        assert actions.dtype == torch.int32 and actions.is_contiguous()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_sim_step(self.h, _ptr(actions), _ptr(self.reward),
+                                             _ptr(self.done), _ptr(self.all_done), _ptr(self.err),
+                                             _stream()), 'gw_sim_step')
+        return self.reward, self.done, self.all_done
+
+    def observe(self, lane, obs=None):
+        """get_obs(lane) in every env (draws in call order); writes obs[:, lane]."""
+        out = self.obs if obs is None else obs
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_observe(self.h, int(lane), _ptr(out), _stream()), 'gw_observe')
+        return out[:, lane]
+
+    def get_aux_state(self):
+        E, A, dev = self.E, self.A, self.device
+        pw = (self.n_passive + 31) // 32
+        st = dict(racc=torch.zeros((E, A), dtype=torch.float64, device=dev),
+                  passive=torch.zeros((E, max(pw, 1)), dtype=torch.int32, device=dev),
+                  turn_pos=torch.full((E,), -1, dtype=torch.int32, device=dev))
+        with torch.cuda.device(dev):
+            _native.check(self.L.gw_get_aux_state(self.h, _ptr(st['racc']), _ptr(st['passive']),
+                                                  _ptr(st['turn_pos']), _stream()),
+                          'gw_get_aux_state')
+        return st
+
+    def set_aux_state(self, racc=None, passive=None, turn_pos=None):
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_set_aux_state(self.h, _ptr(racc), _ptr(passive),
+                                                  _ptr(turn_pos), _stream()), 'gw_set_aux_state')
 
     def random_actions(self, key, step, env_offset=0, out=None):
         """Synthetic random policy (Philox, keyed by key / global env / step / agent)."""

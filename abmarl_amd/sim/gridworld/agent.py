@@ -189,3 +189,32 @@ class AttackingAgent(ActingAgent, GridWorldAgent):
     def configured(self):
         return super().configured and self.attack_range is not None and \
             self.attack_strength is not None and self.attack_accuracy is not None
+
+
+class OrientationAgent(GridWorldAgent):
+    """agent.py:342-373: orientation 1 left, 2 down, 3 right, 4 up;
+    initial_orientation None means random at reset (OrientationState)."""
+
+    def __init__(self, initial_orientation=None, **kwargs):
+        super().__init__(**kwargs)
+        self.initial_orientation = initial_orientation
+        self._orientation = None
+
+    @property
+    def orientation(self):
+        return self._orientation
+
+    @orientation.setter
+    def orientation(self, value):
+        assert value in range(1, 5), "Orientation must be 1, 2, 3, or 4."
+        self._orientation = value
+
+    @property
+    def initial_orientation(self):
+        return self._initial_orientation
+
+    @initial_orientation.setter
+    def initial_orientation(self, value):
+        if value is not None:
+            assert value in range(1, 5), "Initial orientation must be 1, 2, 3, or 4."
+        self._initial_orientation = value

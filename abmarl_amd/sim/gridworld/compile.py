@@ -14,20 +14,25 @@ lowered here, once, to constant tables:
 from abmarl_amd import _abi
 from abmarl_amd.sim.agent_based_simulation import ObservingAgent, ActingAgent
 from abmarl_amd.sim.gridworld.agent import (
-    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, OrientationAgent)
 from abmarl_amd.sim.gridworld.components import (
-    PositionState, HealthState, BinaryAttackActor, SelectiveAttackActor,
-    PositionCenteredEncodingObserver, ActiveDone, OneTeamRemainingDone, MoveActor)
+    PositionState, HealthState, OrientationState, BinaryAttackActor, SelectiveAttackActor,
+    PositionCenteredEncodingObserver, AbsoluteEncodingObserver, ActiveDone, OneTeamRemainingDone,
+    MoveActor, DriftMoveActor)
 
 
 class UnsupportedConfig(ValueError):
     pass
 
 
-def agent_spec(agent, program_type=None):
+def agent_spec(agent, program_type=None, food_type=None):
     kind = 0
     if program_type is not None and isinstance(agent, program_type):
         kind |= _abi.GW_K_PROGRAM
+    if food_type is not None and isinstance(agent, food_type):
+        kind |= _abi.GW_K_FOOD
+    if isinstance(agent, OrientationAgent):
+        kind |= _abi.GW_K_ORIENTATION
     if isinstance(agent, ObservingAgent):
         kind |= _abi.GW_K_OBSERVING
     if isinstance(agent, ActingAgent):
@@ -57,13 +62,16 @@ def agent_spec(agent, program_type=None):
     s.attack_accuracy = float(getattr(agent, 'attack_accuracy', 0) or 0)
     ih = getattr(agent, 'initial_health', None)
     s.initial_health = -1.0 if ih is None else float(ih)
+    s.initial_orientation = int(getattr(agent, 'initial_orientation', None) or 0)
     return s
 
 
 def compile_sim(sim, program, states, observers, dones, actors, state_order,
-                nav_agent=-1, target_agent=-1, program_type=None):
+                nav_agent=-1, target_agent=-1, program_type=None, food_type=None,
+                pacman_agent=-1, tunnel=(-1, -1, -1, -1), pac_rewards=(0, 0, 0, 0, 0)):
     """program_type: the sim program's own agent class (GW_K_PROGRAM bit),
-    e.g. ReachTheTarget's RunningAgent."""
+    e.g. ReachTheTarget's RunningAgent or Pacman's BaddieAgent; food_type:
+    Pacman's FoodAgent (GW_K_FOOD)."""
     agents = list(sim.agents.values())
     for a in agents:
         if not isinstance(a, GridWorldAgent):
@@ -89,11 +97,23 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
 
     obs_range = 0
     observe_self = True
+    obs_kind = _abi.GW_OBS_POSITION_CENTERED
     pco = [o for o in observers if isinstance(o, PositionCenteredEncodingObserver)]
-    if len(pco) != len(observers) or len(pco) > 1:
-        raise UnsupportedConfig("the engine implements one PositionCenteredEncodingObserver")
+    aeo = [o for o in observers if isinstance(o, AbsoluteEncodingObserver)]
+    if len(pco) + len(aeo) != len(observers) or len(observers) > 1:
+        raise UnsupportedConfig("the engine implements one PositionCenteredEncodingObserver "
+                                "or one AbsoluteEncodingObserver")
+    if any(isinstance(s, OrientationState) for s in states) and program != _abi.GW_SIM_PACMAN:
+        raise UnsupportedConfig("OrientationState runs in the Pacman program only")
     ranges = {a.view_range for a in agents if isinstance(a, GridObservingAgent)}
-    if pco:
+    if aeo:
+        if program != _abi.GW_SIM_PACMAN:
+            raise UnsupportedConfig("AbsoluteEncodingObserver runs in the Pacman program only")
+        if any(a.blocking for a in agents):
+            raise UnsupportedConfig("AbsoluteEncodingObserver with blocking entities has no HIP "
+                                    "implementation")
+        obs_kind = _abi.GW_OBS_ABSOLUTE
+    elif pco:
         observe_self = pco[0].observe_self
         if len(ranges) > 1:
             raise UnsupportedConfig("all GridObservingAgents must share one view_range")
@@ -122,6 +142,8 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
                 if a.attack_range > _abi.GW_MAX_RANGE:
                     raise UnsupportedConfig(f"attack_range > {_abi.GW_MAX_RANGE}")
     for x in actors:
+        if isinstance(x, DriftMoveActor) and program == _abi.GW_SIM_PACMAN:
+            continue
         if not isinstance(x, (BinaryAttackActor, SelectiveAttackActor, MoveActor)):
             raise UnsupportedConfig(f"{type(x).__name__} has no HIP implementation")
 
@@ -139,8 +161,10 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
     order = {'position_health': _abi.GW_ORDER_POSITION_HEALTH,
              'health_position': _abi.GW_ORDER_HEALTH_POSITION}[state_order]
     return _abi.CompiledConfig(
-        sim.grid.rows, sim.grid.cols, [agent_spec(a, program_type) for a in agents], program,
+        sim.grid.rows, sim.grid.cols, [agent_spec(a, program_type, food_type) for a in agents],
+        program,
         sim.grid.overlap_bits(), amap, stacked_attacks=stacked, observe_self=observe_self,
         no_overlap_at_reset=pos_states[0].no_overlap_at_reset, state_order=order,
         done_kind=done_kind, obs_range=obs_range, nav_agent=nav_agent, target_agent=target_agent,
-        attack_kind=attack_kind)
+        attack_kind=attack_kind, obs_kind=obs_kind, pacman_agent=pacman_agent, tunnel=tunnel,
+        pac_rewards=pac_rewards)

@@ -14,7 +14,8 @@ import numpy as np
 
 from abmarl_amd.spaces import Box, Discrete
 from abmarl_amd.sim.gridworld.base import GridWorldBaseComponent
-from abmarl_amd.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent
+from abmarl_amd.sim.gridworld.agent import (
+    GridObservingAgent, MovingAgent, AttackingAgent, OrientationAgent)
 
 
 class _EngineExecuted:
@@ -47,6 +48,10 @@ class PositionState(StateBaseComponent):
 
 class HealthState(StateBaseComponent):
     """state.py:622-641: initial_health or np.random.uniform(0, 1)."""
+
+
+class OrientationState(StateBaseComponent):
+    """state.py:659-675: initial_orientation or np.random.randint(1, 5)."""
 
 
 # ----------------------------------------------------------------- actors
@@ -84,6 +89,30 @@ class MoveActor(ActorBaseComponent):
     @property
     def supported_agent_type(self):
         return MovingAgent
+
+
+class CrossMoveActor(ActorBaseComponent):
+    """actor.py:117-192: Discrete(5) moves: 0 stay, 1 left, 2 down, 3 right, 4 up."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        for agent in self.agents.values():
+            if isinstance(agent, self.supported_agent_type):
+                agent.action_space[self.key] = Discrete(5)
+                agent.null_action[self.key] = 0
+
+    @property
+    def key(self):
+        return 'move'
+
+    @property
+    def supported_agent_type(self):
+        return MovingAgent
+
+
+class DriftMoveActor(CrossMoveActor):
+    """actor.py:195-234: a failed or absent change of direction drifts the
+    agent one cell along its orientation (OrientationAgent + MovingAgent)."""
 
 
 class AttackActorBaseComponent(ActorBaseComponent, ABC):
@@ -169,6 +198,28 @@ class PositionCenteredEncodingObserver(ObserverBaseComponent):
     @property
     def key(self):
         return 'position_centered_encoding'
+
+    @property
+    def supported_agent_type(self):
+        return GridObservingAgent
+
+
+class AbsoluteEncodingObserver(ObserverBaseComponent):
+    """observer.py:55-150: Box(-2, max_encoding, (rows, cols), int); the
+    observer itself is -1, cells outside its view range -2."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        max_encoding = max(agent.encoding for agent in self.agents.values())
+        for agent in self.agents.values():
+            if isinstance(agent, self.supported_agent_type):
+                agent.observation_space[self.key] = Box(
+                    -2, max_encoding, (self.rows, self.cols), int)
+                agent.null_observation[self.key] = -2 * np.ones((self.rows, self.cols), dtype=int)
+
+    @property
+    def key(self):
+        return 'absolute_encoding'
 
     @property
     def supported_agent_type(self):

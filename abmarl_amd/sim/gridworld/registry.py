@@ -4,10 +4,10 @@ Only components the engine can execute are registered; ``register`` of any
 other subclass raises, because the fused step cannot run arbitrary Python.
 """
 from abmarl_amd.sim.gridworld.components import (
-    ActorBaseComponent, MoveActor, BinaryAttackActor, SelectiveAttackActor,
-    DoneBaseComponent, ActiveDone, OneTeamRemainingDone,
-    ObserverBaseComponent, PositionCenteredEncodingObserver,
-    StateBaseComponent, PositionState, HealthState,
+    ActorBaseComponent, MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor,
+    SelectiveAttackActor, DoneBaseComponent, ActiveDone, OneTeamRemainingDone,
+    ObserverBaseComponent, PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
+    StateBaseComponent, PositionState, HealthState, OrientationState,
 )
 
 _subclass_check_mapping = {
@@ -18,10 +18,10 @@ _subclass_check_mapping = {
 }
 
 _registered_components = {
-    'actor': {MoveActor, BinaryAttackActor, SelectiveAttackActor},
+    'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor},
     'done': {ActiveDone, OneTeamRemainingDone},
-    'observer': {PositionCenteredEncodingObserver},
-    'state': {PositionState, HealthState},
+    'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
+    'state': {PositionState, HealthState, OrientationState},
 }
 
 registry = {

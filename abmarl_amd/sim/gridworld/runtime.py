@@ -14,10 +14,16 @@ import torch
 
 from abmarl_amd import _abi
 from abmarl_amd.engine import GridWorldEngine
-from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent
+from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent, OrientationAgent
 
 
 class DictRuntime:
+    """For the Pacman program the manager's protocol stays in Python (the
+    engine's simulation-only entry points): step runs sim.step alone, rewards
+    accumulate on the device until get_reward consumes them, and get_obs draws
+    the observation when it is called, in call order — so the same runtime
+    serves AllStepManager and TurnBasedManager exactly."""
+
     def __init__(self, sim, compiled, device=None):
         self.sim = sim
         self.cc = compiled
@@ -40,6 +46,14 @@ class DictRuntime:
         self.observes = [isinstance(a, GridObservingAgent) for a in sim.agents.values()]
         self.sides = [2 * a.view_range + 1 if isinstance(a, GridObservingAgent) else 0
                       for a in sim.agents.values()]
+        self.lazy = compiled.cfg.sim_kind == _abi.GW_SIM_PACMAN
+        if self.lazy:
+            self.key = 'absolute_encoding'
+            specs = compiled.specs
+            # passive (food) entities, in entity order = passive index order
+            self.passive = [i for i, s in enumerate(specs) if s.kind & _abi.GW_K_FOOD]
+            self.racc = np.zeros(A)
+            self._racc_dirty = False
 
     # -------------------------------------------------------------- RNG sync
     def _push_rng(self):
@@ -54,25 +68,83 @@ class DictRuntime:
 
     def _pull(self):
         st = self.eng.get_state()
+        if self.lazy:
+            aux = self.eng.get_aux_state()
         torch.cuda.synchronize(self.dev)
         host = {k: v.cpu().numpy() for k, v in st.items()}
+        pbits = aux['passive'].cpu().numpy().view(np.uint32)[0] if self.lazy else None
+        food = {}
+        if self.lazy:
+            for k, i in enumerate(self.passive):
+                food[i] = bool((pbits[k >> 5] >> (k & 31)) & 1)
         mt = host['mt'].view(np.uint32)[0]
         np.random.set_state(('MT19937', mt[:624].copy(), int(mt[624])) + tuple(self._gauss))
         flags = host['flags'][0]
         self.live = (flags & _abi.FLAG_LIVE) != 0
         for i, agent in enumerate(self.sim.agents.values()):
             k = self.lane_of[i]
+            if i in food:                  # passive food: on the grid until eaten
+                agent.position = np.array(agent.initial_position, dtype=int)
+                agent._health = 1.0 if food[i] else 0.0
+                agent._active = food[i]
+                continue
             if k < 0:                      # static entity: at its initial position
                 agent.position = np.array(agent.initial_position, dtype=int)
                 agent._active = True
                 continue
+            if isinstance(agent, OrientationAgent):
+                agent._orientation = int((flags[k] >> 3) & 7) or None
             agent.position = host['pos'][0, k].astype(int)
             if isinstance(agent, HealthAgent):
                 agent._health = float(host['health'][0, k])
             agent._active = bool(flags[k] & _abi.FLAG_ACTIVE)
 
+    # ------------------------------------------------- lazy (Pacman) protocol
+    def _push_racc(self):
+        if self._racc_dirty:
+            self.eng.set_aux_state(racc=torch.as_tensor(self.racc[None], device=self.dev))
+            self._racc_dirty = False
+
+    def _lazy_reset(self):
+        self._push_rng()
+        self.eng.err.zero_()
+        self.eng.sim_reset()
+        self.eng.check_errors()
+        self.racc[:] = 0.0
+        self._racc_dirty = False
+        self.all_done = False
+        self._pull()
+
+    def _lazy_step(self, action_dict):
+        act = np.zeros((1, len(self.lanes), self.eng.act_dim), np.int32)
+        act[0, :, 2] = -1                      # not in action_dict
+        for aid, a in action_dict.items():
+            k = self.lane_of[self.index[aid]]
+            assert k >= 0, f"{aid} does not act"
+            a = a if isinstance(a, dict) else {}
+            act[0, k, 0] = int(np.asarray(a.get('move', 0)).reshape(-1)[0])
+            act[0, k, 2] = 0
+        self._push_rng()
+        self._push_racc()
+        self.eng.err.zero_()
+        rew, done, all_done = self.eng.sim_step(torch.as_tensor(act, device=self.dev))
+        self.racc = rew[0].cpu().numpy().copy()
+        self.done = done[0].cpu().numpy().copy()
+        self.all_done = bool(all_done[0].item())
+        self._pull()
+        self.eng.check_errors()
+
+    def _lazy_obs(self, i):
+        self._push_rng()
+        self._push_racc()
+        o = self.eng.observe(self.lane_of[i])[0].cpu().numpy()
+        self._pull()
+        return {self.key: o.astype(int)}
+
     # -------------------------------------------------------------- protocol
     def reset(self):
+        if self.lazy:
+            return self._lazy_reset()
         self._push_rng()
         self.eng.err.zero_()
         obs = self.eng.reset()
@@ -89,6 +161,8 @@ class DictRuntime:
         if order != sorted(order):
             raise NotImplementedError(
                 "the engine processes actions in agents-dict order; got a different order")
+        if self.lazy:
+            return self._lazy_step(action_dict)
         act = np.zeros((1, len(self.lanes), self.eng.act_dim), np.int32)
         act[0, :, 2] = -1                      # not in action_dict: does not act
         for aid, a in action_dict.items():
@@ -113,6 +187,8 @@ class DictRuntime:
         i = self.index[agent_id]
         if not self.observes[i]:
             return {}
+        if self.lazy:
+            return self._lazy_obs(i)
         s = self.sides[i]
         return {self.key: self.obs[self.lane_of[i], :s, :s].astype(int)}
 
@@ -120,6 +196,11 @@ class DictRuntime:
         k = self.lane_of[self.index[agent_id]]
         if k < 0:
             return 0.0
+        if self.lazy:                          # smart.py:101-104: consume the accumulator
+            r = float(self.racc[k])
+            self.racc[k] = 0.0
+            self._racc_dirty = True
+            return r
         r = float(self.reward[k])
         self.reward[k] = 0.0
         return r

@@ -24,6 +24,11 @@
  *               -> MazeNavigationSim.step               examples/sim/maze_navigation.py:25-42
  *               -> get_obs / get_reward / get_done      sim/gridworld/smart.py:93-117
  *                  -> ActiveDone / OneTeamRemainingDone sim/gridworld/done.py:39-56,140-153
+ *               -> PacmanSim.step                     examples/sim/pacman.py:80-135
+ *                  -> DriftMoveActor.process_action   sim/gridworld/actor.py:195-234
+ *               -> AbsoluteEncodingObserver.get_obs   sim/gridworld/observer.py:95-150
+ *   gw_turn_reset / gw_turn_step   TurnBasedManager.reset/step  managers/turn_based_manager.py:22-94
+ *   gw_sim_reset / gw_sim_step / gw_observe   SmartGWS.reset / sim.step / get_obs
  *   gw_get_state / gw_set_state   (no reference equivalent: engine SoA snapshot,
  *               used for checkpoint and for parity tests)
  *   gw_destroy  (Python GC of the simulation objects)
@@ -87,6 +92,9 @@ typedef int32_t gw_status;
 #define GW_ERR_INIT_POSITION  2u  /* PositionState: AssertionError initial cell taken     state.py:147-149 */
 #define GW_ERR_DOUBLE_REMOVE  4u  /* ReachTheTarget: KeyError, Grid.remove of an agent the target
                                      already killed on its own cell (reach_the_target.py:118-120) */
+#define GW_ERR_TUNNEL_PLACE   8u  /* Pacman: Grid.place at the far end of the tunnel refused the
+                                     agent, which is left off the grid (pacman.py:88-93);
+                                     its next move would raise KeyError in Grid.remove */
 
 /* ------------------------------------------------------------ agent kinds */
 /* bit flags describing which reference mixins an entity derives from        */
@@ -98,6 +106,9 @@ typedef int32_t gw_status;
 #define GW_K_HEALTH        0x20u /* HealthAgent               gridworld/agent.py:172         */
 #define GW_K_PROGRAM       0x80u /* the sim program's own agent class (ReachTheTarget:
                                     RunningAgent, reach_the_target.py:75-81)        */
+#define GW_K_ORIENTATION  0x100u /* OrientationAgent          gridworld/agent.py:342-373   */
+#define GW_K_FOOD         0x200u /* Pacman FoodAgent (pacman.py:17-19); with GW_SIM_PACMAN,
+                                    GW_K_PROGRAM marks its BaddieAgent (pacman.py:22-24) */
 #define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75;
                                     active blocking entities mask cells from
                                     observers and attackers (utils.py:5-117) */
@@ -106,6 +117,13 @@ typedef int32_t gw_status;
 #define GW_SIM_TEAM_BATTLE  1   /* examples/sim/team_battle_example.py:33-59 */
 #define GW_SIM_MAZE_NAV     2   /* examples/sim/maze_navigation.py:25-42     */
 #define GW_SIM_REACH_TARGET 3   /* examples/sim/reach_the_target.py:84-158   */
+#define GW_SIM_PACMAN       4   /* examples/sim/pacman.py:29-158: DriftMoveActor moves, the
+                                   tunnel, food and baddies (see "Pacman program" below) */
+
+/* observer of the sim's GridObservingAgents */
+#define GW_OBS_POSITION_CENTERED 0  /* observer.py:153-250: (2v+1)^2 window, -1 off-grid   */
+#define GW_OBS_ABSOLUTE          1  /* observer.py:55-150: rows x cols, -1 = the observer,
+                                       -2 = outside its view range                    */
 
 /* attack actor of the sim */
 #define GW_ATTACK_BINARY     0  /* BinaryAttackActor     actor.py:441-501: one int, 0..simultaneous */
@@ -130,6 +148,7 @@ typedef struct gw_agent_spec {
     double   attack_strength;
     double   attack_accuracy;
     double   initial_health;       /* < 0 means None (uniform(0,1) at reset)   */
+    int32_t  initial_orientation;  /* OrientationAgent: 1..4, 0 = None (randint(1, 5)) */
 } gw_agent_spec;
 
 typedef struct gw_config {
@@ -152,6 +171,11 @@ typedef struct gw_config {
     int32_t  nav_agent;            /* MazeNav: index of 'navigator' (else -1)   */
     const gw_agent_spec* agents;   /* host pointer, n_agents entries            */
     int32_t  attack_kind;          /* GW_ATTACK_*                               */
+    int32_t  obs_kind;             /* GW_OBS_*                                  */
+    /* Pacman program (GW_SIM_PACMAN) */
+    int32_t  pacman_agent;         /* index of 'pacman' (else -1)               */
+    int32_t  tunnel[4];            /* r0, c0, r1, c1: the teleporting cells (pacman.py:88-93) */
+    double   pac_rewards[5];       /* reward_scheme: bad_move, entropy, eat_food, kill, die */
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack
@@ -245,11 +269,60 @@ gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
 gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
                             int32_t* actions, void* stream);
 
+/* ---------------------------------------------------------------------
+ * Pacman program (GW_SIM_PACMAN): the turn-based and simulation-only
+ * protocols.  Entities of GW_K_FOOD are passive (one bit per env, not a
+ * lane); observations are AbsoluteEncodingObserver grids, int32[E][A][rows][cols]
+ * (gw_obs_shape).  Actions: actions[e][a] = {cross_move 0..4, unused, present};
+ * present < 0 marks an agent that is not in the action dict.
+ * ------------------------------------------------------------------- */
+
+/* TurnBasedManager.reset (managers/turn_based_manager.py:22-32) of the envs
+   with mask[e] != 0 (all when NULL): SmartGWS.reset, then the observation of
+   the next agent of the (never restarted) turn cycle only.
+     returned  device uint8[E][A]: 1 for the lane whose obs was written
+     turn      device int32[E]:    the lane whose action the next call takes */
+gw_status gw_turn_reset(gw_handle h, const uint8_t* mask, int32_t* obs, uint8_t* returned,
+                        int32_t* turn, uint32_t* err_flags, void* stream);
+
+/* TurnBasedManager.step (turn_based_manager.py:34-94) with NEXT_STEP
+   auto-reset: the lane turn[e] acts (its action row), then the outputs of the
+   agents the manager returns — the next live agent of the cycle, or every
+   live agent once '__all__' — are written (returned[e][a] = 1); reward is the
+   agent's accumulated reward since it last received one.  An env whose
+   previous call ended it (all_done[e] on input, or steps >= horizon > 0) is
+   reset instead (gw_turn_reset outputs, reward 0, all_done 0).            */
+gw_status gw_turn_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
+                       uint8_t* done, uint8_t* all_done, uint8_t* returned, int32_t* turn,
+                       uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream);
+
+/* The simulation alone, for a manager that lives in the host (the dict API):
+   gw_sim_reset = SmartGWS.reset (no observation drawn); gw_sim_step =
+   sim.step(action_dict) (reward[e][a] = the agent's accumulated reward, not
+   consumed; done = get_done; all_done = get_all_done); gw_observe =
+   get_obs(lane) for every env, drawing in call order (observer.py:131-134). */
+gw_status gw_sim_reset(gw_handle h, const uint8_t* mask, uint32_t* err_flags, void* stream);
+gw_status gw_sim_step(gw_handle h, const int32_t* actions, double* reward, uint8_t* done,
+                      uint8_t* all_done, uint32_t* err_flags, void* stream);
+gw_status gw_observe(gw_handle h, int32_t lane, int32_t* obs, void* stream);
+
+/* Program state beside gw_get_state: reward accumulators double[E][A]
+   (SmartGWS.rewards), passive entities still on the grid uint32[E][ceil(P/32)]
+   (P = gw_num_passive), the turn cycle position int32[E] (-1 before the
+   first reset).  NULL pointers are skipped.                                 */
+gw_status gw_get_aux_state(gw_handle h, double* racc, uint32_t* passive_bits, int32_t* turn_pos,
+                           void* stream);
+gw_status gw_set_aux_state(gw_handle h, const double* racc, const uint32_t* passive_bits,
+                           const int32_t* turn_pos, void* stream);
+
 gw_status gw_destroy(gw_handle h);
 
 /* Introspection */
 int32_t     gw_num_envs(gw_handle h);
 int32_t     gw_obs_side(gw_handle h);
+/* per-lane observation shape: (S, S) position-centred, (rows, cols) absolute */
+gw_status   gw_obs_shape(gw_handle h, int32_t* rows, int32_t* cols);
+int32_t     gw_num_passive(gw_handle h);
 int32_t     gw_num_lanes(gw_handle h);
 int32_t     gw_act_dim(gw_handle h);
 /* entity index (into gw_config.agents) of each lane; out: host int32[A]     */

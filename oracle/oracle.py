@@ -46,6 +46,13 @@ def lib():
         L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
         L.gwo_mt_probe.argtypes = [C.c_uint32, C.c_int32, C.c_uint32, C.c_int32, vp]
+        L.gwo_turn_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.gwo_turn_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.gwo_sim_reset.argtypes = [vp, vp, vp]
+        L.gwo_sim_step.argtypes = [vp, vp, vp, vp]
+        L.gwo_observe.argtypes = [vp, C.c_int32, vp]
+        L.gwo_get_aux.argtypes = [vp, vp, vp, vp]
+        L.gwo_take_reward.argtypes = [vp, C.c_int32, vp]
         _lib = L
     return _lib
 
@@ -75,7 +82,7 @@ class Oracle:
         self.L.gwo_seed(self.h, _p(seeds))
 
     def new_obs(self):
-        return np.full((self.E, self.A, self.S, self.S), -2, dtype=np.int32)
+        return np.full((self.E, self.A) + tuple(self.cc.obs_shape), -2, dtype=np.int32)
 
     def reset(self, obs, mask=None, all_done=None, horizon=0):
         err = np.zeros(self.E, dtype=np.uint32)
@@ -90,6 +97,53 @@ class Oracle:
         mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         self.L.gwo_step_masked(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
                                _p(acting), _p(mask))
+
+    # ---- TurnBasedManager protocol (gwo_turn_*)
+    def turn_reset(self, obs, mask=None):
+        err = np.zeros(self.E, np.uint32)
+        ret = np.zeros((self.E, self.A), np.uint8)
+        turn = np.zeros(self.E, np.int32)
+        mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.gwo_turn_reset(self.h, _p(mask), _p(obs), _p(ret), _p(turn), _p(err))
+        return ret, turn, err
+
+    def turn_step(self, actions, obs, reward, done, all_done, mask=None):
+        actions = np.ascontiguousarray(actions, dtype=np.int32)
+        ret = np.zeros((self.E, self.A), np.uint8)
+        turn = np.zeros(self.E, np.int32)
+        mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.gwo_turn_step(self.h, _p(actions), _p(obs), _p(reward), _p(done), _p(all_done),
+                             _p(ret), _p(turn), _p(mask))
+        return ret, turn
+
+    # ---- the simulation alone (dict API)
+    def sim_reset(self, mask=None):
+        err = np.zeros(self.E, np.uint32)
+        mask = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.gwo_sim_reset(self.h, _p(mask), _p(err))
+        return err
+
+    def sim_step(self, actions):
+        actions = np.ascontiguousarray(actions, dtype=np.int32)
+        done = np.zeros((self.E, self.A), np.uint8)
+        all_done = np.zeros(self.E, np.uint8)
+        self.L.gwo_sim_step(self.h, _p(actions), _p(done), _p(all_done))
+        return done, all_done
+
+    def observe(self, entity, obs):
+        self.L.gwo_observe(self.h, int(entity), _p(obs))
+
+    def aux(self):
+        racc = np.zeros((self.E, self.A), np.float64)
+        orient = np.zeros((self.E, self.A), np.int32)
+        cyc = np.zeros(self.E, np.int32)
+        self.L.gwo_get_aux(self.h, _p(racc), _p(orient), _p(cyc))
+        return dict(racc=racc, orient=orient, cyc=cyc)
+
+    def take_reward(self, entity):
+        out = np.zeros(self.E, np.float64)
+        self.L.gwo_take_reward(self.h, int(entity), _p(out))
+        return out
 
     def errors(self):
         out = np.zeros(self.E, np.uint32)

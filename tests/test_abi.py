@@ -49,16 +49,17 @@ def test_constants_match_header():
 
 
 def test_struct_layout():
-    # gw_agent_spec: 8 int32 + 3 double = 56 bytes; gw_config ends with a pointer
-    assert C.sizeof(_abi.AgentSpec) == 56
+    # gw_agent_spec: 8 int32 + 3 double + int32 (+4 padding) = 64 bytes
+    assert C.sizeof(_abi.AgentSpec) == 64
     assert _abi.Config.agents.offset % 8 == 0
+    assert _abi.Config.pac_rewards.offset % 8 == 0
 
 
 def test_create_rejects_bad_config_without_gpu(lib):
     # argument validation happens before any HIP call
     h = C.c_void_p()
     assert lib.gw_create(None, 4, 0, C.byref(h)) == _abi.GW_E_INVALID
-    assert lib.gw_abi_version() == 2
+    assert lib.gw_abi_version() == 3
 
 
 def test_oracle_exports(oracle_mod):
