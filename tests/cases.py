@@ -11,7 +11,7 @@ from abmarl_amd.sim.gridworld.agent import (
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
-                'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double']
+                'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double', 'rtt_64']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -49,7 +49,7 @@ def build_rtt(c):
             kw['initial_position'] = np.array(corners[i % 4], dtype=int)
         agents[f'runner{i}'] = RunningAgent(id=f'runner{i}', **kw)
     kw = dict(c['target'])
-    if c.get('corners'):
+    if c.get('corners') or c.get('target_center'):
         kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
     agents['target'] = TargetAgent(**kw)
     return ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},

@@ -81,6 +81,13 @@ CASES = [
          n_steps=80, horizon=25, seed_base=44,
          runner=dict(move_range=1, view_range=2, initial_health=1),
          target=dict(view_range=2, attack_range=1, attack_strength=1, attack_accuracy=1)),
+    # BASELINE config 4's size: 64x64, 128 barriers, 127 runners, the target
+    # in the center (as in the reference example); 256 entities, so the
+    # engine runs it on its workgroup-per-env kernel
+    dict(name='rtt_64', kind='rtt', rows=64, cols=64, n_barriers=128, n_runners=127, n_envs=2,
+         n_steps=60, horizon=40, seed_base=64, target_center=True,
+         runner=dict(move_range=2, view_range=3, initial_health=1),
+         target=dict(view_range=3, attack_range=1, attack_strength=1, attack_accuracy=1)),
     # MazeNavigation 16x16 from generate_maze (utils.py:120-212), N and T on passages
     dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
          horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
@@ -196,7 +203,7 @@ def build_reference_rtt(c):
             kw['initial_position'] = np.array(corners[i % 4], dtype=int)
         agents[f'runner{i}'] = RunningAgent(id=f'runner{i}', **kw)
     kw = dict(c['target'])
-    if c.get('corners'):
+    if c.get('corners') or c.get('target_center'):
         kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
     agents['target'] = TargetAgent(**kw)
     sim = ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
