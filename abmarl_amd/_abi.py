@@ -6,6 +6,8 @@ integers (``tensor.data_ptr()``) and streams as ``void*``.
 import ctypes as C
 
 GW_MAX_AGENTS = 64
+GW_MAX_LANES = 256
+GW_KERNEL_WAVE, GW_KERNEL_WORKGROUP, GW_KERNEL_PACMAN = 0, 1, 2
 GW_MAX_ENTITIES = 4096
 GW_MAX_ENC = 15
 GW_MAX_CELLS = 4096

@@ -42,6 +42,7 @@ SIGNATURES = {
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),
     'gw_num_lanes': (_i32, [_vp]),
+    'gw_env_kernel': (_i32, [_vp]),
     'gw_act_dim': (_i32, [_vp]),
     'gw_lane_entities': (_i32, [_vp, _vp]),
     'gw_obs_shape': (_i32, [_vp, _vp, _vp]),
@@ -61,7 +62,8 @@ SIGNATURES = {
 def build(force=False, verbose=False, stamps=False, checks=False):
     """Compile the engine for gfx950 with hipcc (works without a GPU)."""
     out = LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB)
-    deps = [SRC, INCLUDE, os.path.join(os.path.dirname(SRC), 'gw_pacman.inc')]
+    deps = [SRC, INCLUDE, os.path.join(os.path.dirname(SRC), 'gw_pacman.inc'),
+            os.path.join(os.path.dirname(SRC), 'gw_rtt.inc')]
     if not force and os.path.exists(out) and \
             os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out

@@ -123,6 +123,9 @@ struct Params {
     uint8_t* returned;                     // [E][A] lanes in the returned dicts
     int32_t* turn;                         // [E] lane whose action the next call takes
     uint64_t agent_lanes;                  // lanes that are Agents (the turn cycle)
+    // ReachTheTarget on a workgroup per env (gw_rtt.inc)
+    int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
+    int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -525,7 +528,7 @@ __device__ __forceinline__ void load_env(const Params& p, int e, Smem& sm, Rng& 
     ctr = c0;
 }
 
-__device__ __forceinline__ void store_rng(const Params& p, int e, Smem& sm, const Rng& rng, uint32_t ctr)
+__device__ __forceinline__ void store_rng(const Params& p, int e, const Smem& sm, const Rng& rng, uint32_t ctr)
 {
     uint32_t* dst = p.mt + (size_t)e * GW_MT_STRIDE;
     const int l = lane_id();
@@ -1942,16 +1945,22 @@ __device__ __forceinline__ uint4 philox(uint4 ctr, uint2 key)
 // the policy's per-agent constants, packed into the kernel arguments (no
 // dependent global load before the first store): kind | move_range << 8 |
 // attack_range << 16 | simultaneous << 20
-struct PolicySpec { uint32_t w[GW_MAX_AGENTS]; };
+struct PolicySpec { uint32_t w[GW_MAX_LANES]; };
 constexpr int RA_CROSS = 100;   // random_actions_kernel: cross moves (Pacman program)
 
 __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
                                       uint32_t step, uint32_t env_offset, int32_t* actions,
                                       int act_dim, int attack_kind)
 {
-    // one wave per env, one lane per agent (no index division); 16 envs per
-    // workgroup keep the dispatch count at ~one workgroup per CU
-    const int e = blockIdx.x * 16 + (int)(threadIdx.x >> 6), a = threadIdx.x & 63;
+    // A <= 64: one wave per env, one lane per agent (no index division), 16
+    // envs per workgroup; wider envs: one thread per (env, agent)
+    int e, a;
+    if (A <= WAVE) {
+        e = blockIdx.x * 16 + (int)(threadIdx.x >> 6); a = threadIdx.x & 63;
+    } else {
+        const int i = blockIdx.x * blockDim.x + threadIdx.x;
+        e = i / A; a = i - e * A;
+    }
     if (e >= E || a >= A) return;
     const size_t i = (size_t)e * A + a;
     const uint32_t pw = ps.w[a];
@@ -1989,6 +1998,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 }
 
 #include "gw_pacman.inc"
+#include "gw_rtt.inc"
 
 }  // namespace
 
@@ -2003,7 +2013,8 @@ struct gw_engine {
     uint32_t* d_static_bits;
     uint32_t* d_shadow;
     uint32_t* d_smask;
-    int32_t lane_ent[GW_MAX_AGENTS];
+    int32_t lane_ent[GW_MAX_LANES];
+    bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     PolicySpec policy;
     size_t smem_step, smem_reset;
     // Pacman program
@@ -2084,6 +2095,13 @@ static hipError_t launch_reset(const gw_engine* g, const Params& p, hipStream_t 
     return hipGetLastError();
 }
 
+#ifdef GW_ONLY_S   /* diagnostic builds: one window size */
+#define DISPATCH_S(S_, FN, ...)                      \
+    switch (S_) {                                    \
+    case GW_ONLY_S: return FN<GW_ONLY_S>(__VA_ARGS__); \
+    default: return hipErrorInvalidValue;            \
+    }
+#else
 #define DISPATCH_S(S_, FN, ...)                      \
     switch (S_) {                                    \
     case 1: return FN<1>(__VA_ARGS__);               \
@@ -2096,6 +2114,36 @@ static hipError_t launch_reset(const gw_engine* g, const Params& p, hipStream_t 
     case 15: return FN<15>(__VA_ARGS__);             \
     default: return hipErrorInvalidValue;            \
     }
+#endif
+
+template <int S>
+static hipError_t launch_wg_step(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(wg_step_kernel<S>, dim3(g->E), dim3(WAVE * p.nwv), g->smem_step, st, p);
+    return hipGetLastError();
+}
+
+template <int S>
+static hipError_t launch_wg_reset(const gw_engine* g, const Params& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(g->E), dim3(WAVE * p.nwv), g->smem_reset, st, p);
+    return hipGetLastError();
+}
+
+template <int S>
+static hipError_t set_wg_attr(size_t b)
+{
+    hipError_t e = hipFuncSetAttribute((const void*)wg_step_kernel<S>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)wg_reset_kernel<S>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
+}
+
+static hipError_t set_wg_attrs(int S, size_t b)
+{
+    DISPATCH_S(S, set_wg_attr, b);
+}
 
 static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st)
 {
@@ -2106,12 +2154,14 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
+    if (g->wg) { DISPATCH_S(g->S, launch_wg_step, g, p, st); }
     DISPATCH_S(g->S, launch_step, g, p, st);
 }
 
 static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_RESET_ALL; return launch_pac(g, p, st); }
+    if (g->wg) { DISPATCH_S(g->S, launch_wg_reset, g, p, st); }
     DISPATCH_S(g->S, launch_reset, g, p, st);
 }
 
@@ -2235,8 +2285,16 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         (st ? statics : lanes).push_back(a);
     }
     const int A = (int)lanes.size();
-    if (A == 0 || A > GW_MAX_AGENTS) {
-        set_err("%d dynamic entities outside 1..%d (one wavefront lane each)", A, GW_MAX_AGENTS);
+    // ReachTheTarget runs on a workgroup per env when it has more lanes than a
+    // wave (or when GW_RTT_KERNEL=wg asks for it: the parity tests run the
+    // small reference fixtures through it)
+    const char* rk = getenv("GW_RTT_KERNEL");
+    const bool wg = rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE &&
+                    (A > GW_MAX_AGENTS || (rk && strcmp(rk, "wg") == 0));
+    const int max_lanes = wg ? GW_MAX_LANES : GW_MAX_AGENTS;
+    if (A == 0 || A > max_lanes) {
+        set_err("%d dynamic entities outside 1..%d (%s)", A, max_lanes,
+                rtt ? "ReachTheTarget: one thread each, SelectiveAttackActor" : "one wavefront lane each");
         return GW_E_UNSUPPORTED;
     }
     if ((int)passive.size() > 32 * PAC_MAX_PWORDS) {
@@ -2269,6 +2327,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     g->device = device; g->E = n_envs; g->A = A; g->H = cfg->rows; g->W = cfg->cols;
     g->S = pac ? 1 : 2 * cfg->obs_range + 1; g->max_enc = max_enc;
     g->pacman = pac;
+    g->wg = wg;
     for (int i = 0; i < A; i++) g->lane_ent[i] = lanes[i];
     const size_t EA = (size_t)n_envs * A;
     Params& p = g->base;
@@ -2284,7 +2343,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     HIPCHK(hipMemset(p.seq, 0, EA * sizeof(uint32_t)));
     HIPCHK(hipMemset(p.mt, 0, (size_t)n_envs * GW_MT_STRIDE * sizeof(uint32_t)));
     HIPCHK(hipMemset(p.steps, 0, (size_t)n_envs * sizeof(int32_t)));
-    DevAgent hs[GW_MAX_AGENTS];
+    DevAgent hs[GW_MAX_LANES];
     for (int l = 0; l < A; l++) {
         const gw_agent_spec& s = cfg->agents[lanes[l]];
         hs[l].enc = s.encoding; hs[l].kind = s.kind; hs[l].init_r = s.init_row; hs[l].init_c = s.init_col;
@@ -2294,7 +2353,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].init_health = s.initial_health;
         hs[l].init_orient = s.initial_orientation;
     }
-    for (int l = 0; l < GW_MAX_AGENTS; l++) {
+    for (int l = 0; l < GW_MAX_LANES; l++) {
         g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
                                   ((uint32_t)(hs[l].attack_range & 0xf) << 16) |
                                   ((uint32_t)(hs[l].simul & 0xfff) << 20)) : 0u;
@@ -2419,6 +2478,17 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         if (pw > wb) g->smem_step += pw - wb;
     }
     g->smem_reset = g->smem_step;
+    if (wg) {
+        p.nwv = (A + WAVE - 1) / WAVE;
+        g->smem_step = g->smem_reset = wg_smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
+        // moves run in parallel when every moving lane's encoding may share a
+        // cell with every lane encoding (static cells are refused separately)
+        uint32_t lane_encs = 0;
+        for (int l = 0; l < A; l++) lane_encs |= 1u << hs[l].enc;
+        p.par_moves = 1;
+        for (int l = 0; l < A; l++)
+            if ((hs[l].kind & GW_K_MOVING) && (p.overlap[hs[l].enc] & lane_encs) != lane_encs) p.par_moves = 0;
+    }
     if (g->smem_step > 160 * 1024) { set_err("LDS need %zu B > 160 KiB", g->smem_step); return GW_E_UNSUPPORTED; }
     if (pac) {
         p.obs_kind = cfg->obs_kind;
@@ -2456,7 +2526,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
     HIPCHK(hipMemset(p.racc, 0, EA * sizeof(double)));
-    HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
+    if (wg) HIPCHK(set_wg_attrs(g->S, g->smem_step));
+    else HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
     *out = g;
     return GW_OK;
 }
@@ -2477,6 +2548,10 @@ gw_status gw_destroy(gw_handle g)
 int32_t gw_num_envs(gw_handle g) { return g ? g->E : 0; }
 int32_t gw_obs_side(gw_handle g) { return g ? g->S : 0; }
 int32_t gw_num_lanes(gw_handle g) { return g ? g->A : 0; }
+int32_t gw_env_kernel(gw_handle g)
+{
+    return !g ? -1 : g->pacman ? GW_KERNEL_PACMAN : g->wg ? GW_KERNEL_WORKGROUP : GW_KERNEL_WAVE;
+}
 int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
 
 gw_status gw_lane_entities(gw_handle g, int32_t* out)
@@ -2699,7 +2774,8 @@ gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t e
                             int32_t* actions, void* stream)
 {
     if (!g || !actions) return GW_E_INVALID;
-    hipLaunchKernelGGL(random_actions_kernel, dim3((g->E + 15) / 16), dim3(16 * WAVE), 0,
+    const dim3 grid = g->A <= WAVE ? dim3((g->E + 15) / 16) : dim3((unsigned)(((size_t)g->E * g->A + 255) / 256));
+    hipLaunchKernelGGL(random_actions_kernel, grid, dim3(g->A <= WAVE ? 16 * WAVE : 256), 0,
                        (hipStream_t)stream, g->policy, g->E, g->A, key, step, env_offset, actions,
                        g->base.act_dim, g->pacman ? RA_CROSS : g->base.attack_kind);
     HIPCHK(hipGetLastError());

@@ -53,7 +53,8 @@
  *       observe, and no other entity can share their cell, so they live in
  *       the per-config cell-table template (and block sight when blocking);
  *     lanes: every other entity, at most GW_MAX_AGENTS (one wavefront lane
- *       each).
+ *       each), or GW_MAX_LANES for the ReachTheTarget program, which runs on
+ *       one workgroup per env when it has more than GW_MAX_AGENTS lanes.
  *   Every per-entity array below ([E][A]...) is indexed by LANE, A =
  *   gw_num_lanes(h); gw_lane_entities gives the entity index of each lane.
  *   Static entities sit at their initial position, active, in every env.
@@ -69,6 +70,9 @@ extern "C" {
 
 /* ------------------------------------------------------------------ limits */
 #define GW_MAX_AGENTS   64   /* lanes: one wavefront lane per dynamic entity  */
+#define GW_MAX_LANES   256   /* ReachTheTarget program with SelectiveAttackActor:
+                                one workgroup per env, one thread per dynamic
+                                entity (BASELINE config 4: 256 entities)      */
 #define GW_MAX_ENTITIES 4096 /* lanes + static entities                       */
 #define GW_MAX_ENC      15   /* encodings 1..15                               */
 #define GW_MAX_CELLS  4096   /* rows*cols                                     */
@@ -324,6 +328,13 @@ int32_t     gw_obs_side(gw_handle h);
 gw_status   gw_obs_shape(gw_handle h, int32_t* rows, int32_t* cols);
 int32_t     gw_num_passive(gw_handle h);
 int32_t     gw_num_lanes(gw_handle h);
+/* the step kernel's execution model: GW_KERNEL_WAVE (one wavefront per env),
+   GW_KERNEL_WORKGROUP (ReachTheTarget: one workgroup of ceil(A/64) waves per
+   env), GW_KERNEL_PACMAN (the Pacman program, one wavefront per env)         */
+#define GW_KERNEL_WAVE      0
+#define GW_KERNEL_WORKGROUP 1
+#define GW_KERNEL_PACMAN    2
+int32_t     gw_env_kernel(gw_handle h);
 int32_t     gw_act_dim(gw_handle h);
 /* entity index (into gw_config.agents) of each lane; out: host int32[A]     */
 gw_status   gw_lane_entities(gw_handle h, int32_t* out);

@@ -52,8 +52,17 @@ def build_rtt(c):
     if c.get('corners') or c.get('target_center'):
         kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
     agents['target'] = TargetAgent(**kw)
-    return ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
-                                       attack_mapping={2: {3}})
+    ov = {int(k): set(v) for k, v in c['overlapping'].items()} if 'overlapping' in c \
+        else {2: {3}, 3: {1, 2, 3}}
+    return ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping=ov, attack_mapping={2: {3}})
+
+
+# BASELINE config 4: ReachTheTarget 64x64, 128 barriers + 127 runners + the
+# target (256 entities), the reference example's agent parameters
+# (examples/rllib_reach_the_target.py), the target in the center
+RTT_CONFIG4 = dict(kind='rtt', rows=64, cols=64, n_barriers=128, n_runners=127, target_center=True,
+                   runner=dict(move_range=2, view_range=3, initial_health=1),
+                   target=dict(view_range=3, attack_range=1, attack_strength=1, attack_accuracy=1))
 
 
 def build_sim(c):

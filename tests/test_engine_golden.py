@@ -100,3 +100,16 @@ def test_engine_autoreset_matches_reference(name):
         assert (rew.view(np.uint64) == g['reward'][t].view(np.uint64)).all(), f"step {t}: reward"
         assert (done == g['done'][t]).all() and (ad == g['all_done'][t]).all(), f"step {t}: done"
     assert not eng.err.any().item()
+
+
+RTT_GOLDEN = [n for n in GOLDEN_CASES if n.startswith('rtt')]
+
+
+@pytest.mark.parametrize('name', RTT_GOLDEN)
+def test_engine_workgroup_kernel_matches_reference(name, monkeypatch):
+    """The ReachTheTarget workgroup-per-env kernel (gw_rtt.inc) on every RTT
+    fixture, the small ones included (GW_RTT_KERNEL=wg; config 4's size takes
+    it anyway)."""
+    monkeypatch.setenv('GW_RTT_KERNEL', 'wg')
+    g = load_golden(name)
+    replay(EngineRunner(g), g)
