@@ -1767,13 +1767,21 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
             if (rl(L.r, a) == tr && rl(L.c, a) == tc) {
                 if (!rlb(L.in_grid, a)) {
                     // Grid.remove raises KeyError: the step stops here (no
-                    // further moves, no observation draws); the env needs a reset
+                    // further moves, no observation draws); the env needs a
+                    // reset, which the auto-reset modes do as for an ended
+                    // episode (all_done set; SAME_STEP resets it right away)
                     if (l == 0) {
                         if (p.err) p.err[e] |= GW_ERR_DOUBLE_REMOVE;
                         p.steps[e] = steps0 + 1;
                         if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
+                        if (p.autoreset) p.all_done[e] = 1;
                     }
                     ctr += (uint32_t)WAVE;
+                    if (p.autoreset == 1) {
+                        // the table is not the post-move grid: rebuild from the template
+                        wave_sync();
+                        reset_env<S>(p, e, sm, rng, L, ctr, false);
+                    }
                     store_lane(p, e, L, valid);
                     store_rng(p, e, sm, rng, ctr);
                     return;

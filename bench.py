@@ -63,6 +63,14 @@ def pacman_sim():
     return build_pacman()
 
 
+def rtt_sim():
+    """BASELINE config 4: ReachTheTarget 64x64, 128 barriers + 127 runners +
+    the target (256 entities, the workgroup-per-env kernel)."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from tests.cases import build_rtt, RTT_CONFIG4
+    return build_rtt(dict(RTT_CONFIG4))
+
+
 def pacman_turn_bytes(E, A, HW, pwords):
     """Algorithmic HBM bytes of one turn-based Pacman launch: actions read
     (move + present, 8 B per lane), ONE lane's absolute observation 4*HW,
@@ -81,6 +89,12 @@ def step_bytes(E, A, S):
     per_slot = 12 + 4 * S * S + 8 + 1 + 2 * (8 + 4 + 8 + 1)
     per_env = 1 + 8 + 16 + 16
     return E * (A * per_slot + per_env)
+
+
+def rtt_step_bytes(E, A, S, act_dim):
+    """step_bytes with the SelectiveAttackActor's wider action rows
+    (4 * act_dim B per entity slot instead of 12)."""
+    return step_bytes(E, A, S) + E * A * (4 * act_dim - 12)
 
 
 def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200, mode='next_step'):
@@ -127,10 +141,12 @@ def quick_config(name, steps=200, warmup=20):
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     if name == 'maze':
         cc, E, horizon = maze_sim().compiled(), 1024, 200
+    elif name.startswith('rtt'):
+        cc, E, horizon = rtt_sim().compiled(), (8192 if name == 'rtt_8192' else 1024), 200
     else:
         cc, E, horizon = pacman_sim().compiled(), 16384, 200
     eng = GridWorldEngine(cc, E, seeds=env_seeds(E))
-    if name == 'maze':
+    if name == 'maze' or name.startswith('rtt'):
         eng.reset()
         eng.all_done.zero_()
         step = lambda: eng.step_autoreset_next(horizon=horizon)
@@ -159,6 +175,12 @@ def quick_config(name, steps=200, warmup=20):
     if name == 'maze':
         nbytes = step_bytes(E, eng.A, cc.obs_side)
         desc = 'MazeNavigation 16x16 (maze_16 fixture map), 1024 envs, AllStep, next_step auto-reset'
+    elif name.startswith('rtt'):
+        nbytes = rtt_step_bytes(E, eng.A, cc.obs_side, eng.act_dim)
+        desc = (f'ReachTheTarget 64x64, 128 barriers + 127 runners + target (256 entities, '
+                f'workgroup-per-env kernel), {E} envs on one GPU '
+                f'({"all of config 4" if E == 8192 else "one GPU share of config 4 8192 envs / 8"}), '
+                'AllStep, horizon 200, next_step auto-reset')
     else:
         nbytes = pacman_turn_bytes(E, eng.A, cc.rows * cc.cols, (eng.n_passive + 31) // 32)
         desc = ('Pacman pacman.txt, 4 baddies + pacman, 16384 envs, TurnBasedManager protocol '
@@ -296,6 +318,8 @@ def main():
         if world == 1 and not args.no_other:
             # BASELINE configs 2 and 5 (single GPU, short runs; not the metric)
             out['other_configs'] = {'maze_16': quick_config('maze'),
+                                    'reach_the_target_64': quick_config('rtt'),
+                                    'reach_the_target_64_all_8192': quick_config('rtt_8192'),
                                     'pacman_turn_based': quick_config('pacman')}
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds, horizon=args.horizon,

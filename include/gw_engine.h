@@ -227,7 +227,10 @@ gw_status gw_reset(gw_handle h, const uint8_t* mask, const uint8_t* all_done,
      all_done  device uint8[E]          ('__all__')
      acting    device uint64[E] or NULL (+= number of acting agents, for metrics)
      err_flags device uint32[E] or NULL (|= GW_ERR_*: a step the reference
-               would raise in; that env's outputs are not written)          */
+               would raise in; that env's outputs are not written.  In the
+               auto-reset calls below such an env is reset like one whose
+               episode ended: all_done[e] = 1, and gw_step_autoreset writes
+               the next episode's first observation in the same launch)     */
 gw_status gw_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
                   uint8_t* done, uint8_t* all_done, uint64_t* acting, uint32_t* err_flags,
                   void* stream);
