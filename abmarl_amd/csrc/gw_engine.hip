@@ -126,6 +126,7 @@ struct Params {
     // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
+    int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -2496,6 +2497,25 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         p.par_moves = 1;
         for (int l = 0; l < A; l++)
             if ((hs[l].kind & GW_K_MOVING) && (p.overlap[hs[l].enc] & lane_encs) != lane_encs) p.par_moves = 0;
+        // parallel placement needs every list length to follow from the
+        // placement order: no two lanes that can share a cell at reset may
+        // both remove it from one list (a removal would then not shorten it)
+        const uint32_t all_encs = ((2u << max_enc) - 1u) & ~1u;
+        auto rmv = [&](int enc) { return cfg->no_overlap_at_reset ? all_encs : (all_encs & ~p.overlap[enc]); };
+        p.place_par = 1;
+        for (int a = 1; a <= max_enc; a++) {
+            if (!((lane_encs >> a) & 1u)) continue;
+            for (int b = 1; b <= max_enc; b++) {
+                if (!((lane_encs >> b) & 1u)) continue;
+                // b placed after a can land on a's cell iff b's list kept it
+                if (!((rmv(a) >> b) & 1u) && (rmv(a) & rmv(b))) p.place_par = 0;
+            }
+        }
+        for (int a = 0; a < A; a++)
+            for (int b = a + 1; b < A; b++)
+                if (hs[a].init_r >= 0 && hs[a].init_r == hs[b].init_r && hs[a].init_c == hs[b].init_c)
+                    p.place_par = 0;                         // initial positions shared: sequential
+
     }
     if (g->smem_step > 160 * 1024) { set_err("LDS need %zu B > 160 KiB", g->smem_step); return GW_E_UNSUPPORTED; }
     if (pac) {

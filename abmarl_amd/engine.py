@@ -67,6 +67,12 @@ class GridWorldEngine:
         self.act_dim = int(self.L.gw_act_dim(self.h))
         self.actions = torch.zeros((E, A, self.act_dim), dtype=torch.int32, device=dev)
         self._dbg = None
+        self.stamps = None
+        if _native.VARIANT == 'stamps':
+            # per-env s_memtime per phase (diagnostic build, tools/stamps.py)
+            self.stamps = torch.zeros((E, 32), dtype=torch.int64, device=dev)
+            self.L.gw_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+            self.L.gw_debug_set_stamps(self.h, _ptr(self.stamps))
         if _native.VARIANT == 'checks':
             self._dbg = torch.zeros(16, dtype=torch.int32, device=dev)
             self.L.gw_debug_set_checks.argtypes = [C.c_void_p, C.c_void_p]
@@ -229,8 +235,10 @@ class GridWorldEngine:
                                                    _stream()), 'gw_random_actions')
         return out
 
-    def check_errors(self):
-        err = self.err.cpu().numpy()
+    def check_errors(self, allow=0):
+        """Raise the reference's exception for the first env whose err flags
+        (other than the `allow` bits) are set."""
+        err = self.err.cpu().numpy() & ~np.uint32(allow)
         if (err & _abi.GW_ERR_NO_CELL).any():
             e = int(np.nonzero(err & _abi.GW_ERR_NO_CELL)[0][0])
             raise RuntimeError(f"Could not find a cell for an agent (env {e})")

@@ -203,6 +203,10 @@ def main():
     ap.add_argument('--autoreset', choices=['next_step', 'same_step'], default='next_step')
     ap.add_argument('--no-other', action='store_true',
                     help='skip the other auto-reset mode and the other configs')
+    ap.add_argument('--workload', choices=['team_battle', 'rtt'], default='team_battle',
+                    help="'rtt': BASELINE config 4 (ReachTheTarget 64x64, 256 entities; "
+                         "--envs 1024 = one GPU's share of 8192) as the timed workload, "
+                         "for profiling its kernel (not the headline metric)")
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -214,10 +218,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
+    from abmarl_amd import _abi
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     from abmarl_amd.parallel import shard_envs, gather_episode_stats
-    sim = team_battle_sim()
+    sim = team_battle_sim() if args.workload == 'team_battle' else rtt_sim()
     cc = sim.compiled()
+    if args.workload == 'rtt' and args.envs == 4096:
+        args.envs = 1024
     first, E_local = shard_envs(args.envs * world, rank, world)
     key = 0x5eed0000  # policy key shared by all ranks; global env ids make streams distinct
 
@@ -241,7 +248,9 @@ def main():
         for t in range(args.warmup):
             one_step(t)
         torch.cuda.synchronize()
-        eng.check_errors()
+        # ReachTheTarget: a runner placed on the target's cell and killed there
+        # raises the reference's KeyError; the auto-reset modes reset that env
+        eng.check_errors(allow=_abi.GW_ERR_DOUBLE_REMOVE if args.workload == 'rtt' else 0)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
         acting0 = int(eng.acting.sum().item())
@@ -279,9 +288,18 @@ def main():
     if rank == 0:
         value = acting_all / dt_all
         nbytes = step_bytes(E_local, A, S)
+        kname = 'step_kernel<7>'
+        workload = ('TeamBattle 32x32, 64 agents / 2 teams, 4096 envs per GPU, '
+                    f'horizon 200, {args.autoreset} auto-reset')
+        if args.workload == 'rtt':
+            nbytes = rtt_step_bytes(E_local, A, S, cc.act_dim)
+            kname = 'wg_step_kernel<7>'
+            workload = (f'ReachTheTarget 64x64 (BASELINE config 4), 256 entities, {E_local} envs per GPU, '
+                        f'horizon 200, {args.autoreset} auto-reset (profiling run, not the headline metric)')
         achieved = nbytes / (step_ms * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, 'profiles', 'pmc_step_kernel.json')
+        pmc = os.path.join(ROOT, 'profiles', 'pmc_step_kernel.json' if args.workload == 'team_battle'
+                           else 'pmc_wg_step_kernel.json')
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
         out = {
@@ -297,15 +315,14 @@ def main():
             'vs_baseline': None,
             'dtype': 'int32 (positions/obs), f64 (health/reward)',
             'data': 'synthetic: Philox random-policy actions, random-init TeamBattle episodes',
-            'config': {'workload': 'TeamBattle 32x32, 64 agents / 2 teams, 4096 envs per GPU, '
-                                   f'horizon 200, {args.autoreset} auto-reset',
+            'config': {'workload': workload,
                        'envs_per_gpu': E_local, 'global_envs': int(envs_all),
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
             'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                         'traffic': traffic, 'kernel': 'step_kernel<7>',
+                         'traffic': traffic, 'kernel': kname,
                          'kernel_ms': round(step_ms_all, 4),
                          'bytes_per_launch': nbytes},
             'episode_stats': stats,
@@ -315,13 +332,13 @@ def main():
                 'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
                 'kernel_ms': round(r2['step_ms_max'], 4)},
         }
-        if world == 1 and not args.no_other:
+        if world == 1 and not args.no_other and args.workload == 'team_battle':
             # BASELINE configs 2 and 5 (single GPU, short runs; not the metric)
             out['other_configs'] = {'maze_16': quick_config('maze'),
                                     'reach_the_target_64': quick_config('rtt'),
                                     'reach_the_target_64_all_8192': quick_config('rtt_8192'),
                                     'pacman_turn_based': quick_config('pacman')}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == 'team_battle':
             out['cpu_baseline'] = cpu_baseline(cc, seconds=args.cpu_seconds, horizon=args.horizon,
                                                mode=args.autoreset)
         print(json.dumps(out), flush=True)

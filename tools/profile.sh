@@ -1,13 +1,25 @@
 #!/bin/bash
-# rocprofv3 kernel trace + stats and separate PMC passes (FETCH_SIZE, WRITE_SIZE)
-# usage: bash tools/profile.sh <tag>   (writes gpurun_out/prof_<tag>/)
+# rocprofv3 evidence for one bench workload, on the GPU box:
+#   tools/profile.sh <tag> [team_battle|rtt]
+# 1. --kernel-trace --stats over a bench run (per-kernel durations);
+# 2. two separate --pmc passes, FETCH_SIZE and WRITE_SIZE (they do not fit
+#    one pass on gfx950), over a short run of the same workload.
+# Raw outputs go under gpurun_out/prof_<tag>_*; tools/summarize_profile.py
+# turns them into profiles/<tag>_*.
 set -o pipefail
-TAG=${1:-r01}
-OUT=gpurun_out/prof_$TAG
-mkdir -p $OUT
+TAG=${1:?tag}
+WL=${2:-team_battle}
+ROOT=$(pwd)
 export TMPDIR=/tmp
-BENCH="python3 bench.py --no-cpu-baseline --no-other"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH --steps 200 --warmup 20 > $OUT/trace.log 2>&1 || { echo TRACE FAIL; tail -20 $OUT/trace.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $BENCH --steps 30 --warmup 5 > $OUT/fetch.log 2>&1 || { echo FETCH FAIL; tail -20 $OUT/fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $BENCH --steps 30 --warmup 5 > $OUT/write.log 2>&1 || { echo WRITE FAIL; tail -20 $OUT/write.log; exit 1; }
-find $OUT -name '*.csv' | head -20
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+BENCH="$ROOT/bench.py --workload $WL --no-cpu-baseline --no-other"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}_stats" -o run \
+    -- python3 $BENCH --steps 200 --warmup 20 > "$OUT/prof_${TAG}_stats.log" 2>&1 \
+    || { echo "stats pass failed"; tail -20 "$OUT/prof_${TAG}_stats.log"; exit 1; }
+for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/prof_${TAG}_$C" -o run \
+        -- python3 $BENCH --steps 30 --warmup 5 > "$OUT/prof_${TAG}_$C.log" 2>&1 \
+        || { echo "$C pass failed"; tail -20 "$OUT/prof_${TAG}_$C.log"; exit 1; }
+done
+python3 "$ROOT/tools/summarize_profile.py" "$TAG" "$WL" --raw "$OUT" --dest "$OUT/profiles_$TAG"

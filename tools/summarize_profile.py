@@ -1,87 +1,105 @@
-"""Copy a rocprofv3 run (gpurun_out/prof_<tag>/) into profiles/ and derive the
-per-launch HBM traffic of the step kernel from the PMC passes.
+"""Summarize tools/profile.sh output into profiles/<tag>_*:
 
-rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB per dispatch (derived from
-TCC_EA0_RDREQ/WRREQ).  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reads
-half the bytes of 16-B-per-lane streaming loads; WRITE_SIZE is exact for
-16-B-per-lane stores.  The step kernel's loads are mostly 4-8 B per lane
-(uncalibrated widths), so the raw sum is reported together with the
-algorithmic byte count; see DESIGN.md §Roofline.
+  <tag>_<wl>_kernel_stats.csv   rocprofv3 --stats table (copied)
+  <tag>_<wl>_summary.md         per-kernel calls / avg / min / max / share,
+                                the step kernel's resources, PMC traffic
+  pmc_<kernel>.json             FETCH_SIZE / WRITE_SIZE per step launch:
+                                raw (KiB -> bytes) and the gfx950-corrected
+                                HBM bytes (MI355X_MICROARCH.md §HBM: FETCH_SIZE
+                                reports half the bytes of coalesced reads, so
+                                it is doubled; WRITE_SIZE is exact for 16-B
+                                stores) -- bench.py reports hbm_bytes_per_launch
+                                as roofline.traffic.
 
-usage: python tools/summarize_profile.py <tag> [kernel-substring]
+usage: python tools/summarize_profile.py <tag> <team_battle|rtt> --raw DIR --dest DIR
 """
-import collections
+import argparse
 import csv
+import glob
 import json
 import os
 import shutil
-import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = {'team_battle': 'step_kernel<7>', 'rtt': 'wg_step_kernel<7>'}
 
 
-def short_name(n):
-    """'void (anonymous namespace)::step_kernel<7>((anonymous namespace)::Params)'
-    -> 'step_kernel<7>'"""
-    n = n.replace('(anonymous namespace)::', '')
-    if n.startswith('void '):
-        n = n[5:]
+def find(root, pattern):
+    hits = sorted(glob.glob(os.path.join(root, '**', pattern), recursive=True))
+    if not hits:
+        raise SystemExit(f'no {pattern} under {root}')
+    return hits[0]
+
+
+def short(name):
+    n = name.replace('(anonymous namespace)::', '').replace('void ', '')
     return n.split('(')[0][:60]
 
 
-def main():
-    tag = sys.argv[1]
-    kname = sys.argv[2] if len(sys.argv) > 2 else 'step_kernel'
-    src = os.path.join(ROOT, 'gpurun_out', f'prof_{tag}')
-    dst = os.path.join(ROOT, 'profiles')
-    os.makedirs(dst, exist_ok=True)
-    stats = os.path.join(src, 'trace', 'run_kernel_stats.csv')
-    shutil.copy(stats, os.path.join(dst, f'{tag}_kernel_stats.csv'))
-    rows = list(csv.DictReader(open(stats)))
-    trace = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_trace.csv'))))
-    res = {}
-    for r in trace:
-        if kname in short_name(r['Kernel_Name']):
-            res = {k: r.get(k, '') for k in ('LDS_Block_Size', 'Scratch_Size', 'VGPR_Count',
-                                     'Accum_VGPR_Count', 'SGPR_Count', 'Workgroup_Size_X',
-                                     'Grid_Size_X')}
-            break
-    pmc = {}
-    for kind, counter in (('fetch', 'FETCH_SIZE'), ('write', 'WRITE_SIZE')):
-        f = os.path.join(src, kind, 'run_counter_collection.csv')
-        if not os.path.exists(f):
+def pmc_per_launch(root, counter, kernel):
+    path = find(root, '*counter_collection.csv')
+    vals = []
+    for row in csv.DictReader(open(path)):
+        if row.get('Counter_Name') != counter:
             continue
-        vals = collections.defaultdict(list)
-        for r in csv.DictReader(open(f)):
-            if r['Counter_Name'] == counter:
-                vals[r['Kernel_Name']].append(float(r['Counter_Value']))
-        for name, v in vals.items():
-            if kname in name:
-                pmc[counter] = sum(v) / len(v)
-    lines = [f"# rocprofv3 summary `{tag}`", "",
-             "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
-             "--no-cpu-baseline --no-other --steps 200 --warmup 20` (next_step auto-reset; PMC passes: `--pmc FETCH_SIZE` and "
-             "`--pmc WRITE_SIZE`, separate runs, `--steps 30 --warmup 5`).", "",
-             "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
-    for r in rows[:8]:
-        n = short_name(r['Name'])
-        lines.append(f"| `{n}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
-                     f"{float(r['MinNs'])/1e3:.2f} | {float(r['MaxNs'])/1e3:.2f} | "
-                     f"{float(r['Percentage']):.1f} |")
-    lines += ["", f"{kname} resources: `{res}`", ""]
-    out = {'tag': tag, 'kernel': kname, 'resources': res}
-    if pmc:
-        fetch_b = pmc.get('FETCH_SIZE', 0) * 1024
-        write_b = pmc.get('WRITE_SIZE', 0) * 1024
-        out.update(fetch_bytes_per_launch=fetch_b, write_bytes_per_launch=write_b,
-                   hbm_bytes_per_launch=fetch_b + write_b)
-        lines += [f"PMC per {kname} launch: FETCH_SIZE {fetch_b/1e6:.2f} MB, WRITE_SIZE "
-                  f"{write_b/1e6:.2f} MB, sum {(fetch_b+write_b)/1e6:.2f} MB (raw, uncorrected)."]
+        if short(row['Kernel_Name']) != kernel:
+            continue
+        vals.append(float(row['Counter_Value']))
+    if not vals:
+        raise SystemExit(f'{counter}: no {kernel} dispatches in {path}')
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('tag')
+    ap.add_argument('workload', choices=list(KERNEL))
+    ap.add_argument('--raw', required=True)
+    ap.add_argument('--dest', required=True)
+    a = ap.parse_args()
+    kernel = KERNEL[a.workload]
+    os.makedirs(a.dest, exist_ok=True)
+    sroot = os.path.join(a.raw, f'prof_{a.tag}_stats')
+    stats = find(sroot, '*kernel_stats.csv')
+    base = f'{a.tag}_{a.workload}'
+    shutil.copy(stats, os.path.join(a.dest, base + '_kernel_stats.csv'))
+    rows = list(csv.DictReader(open(stats)))
+    res = {}
+    try:
+        trace = find(sroot, '*kernel_trace.csv')
+        for r in csv.DictReader(open(trace)):
+            if short(r['Kernel_Name']) == kernel:
+                res = {k: r[k] for k in ('LDS_Block_Size', 'Scratch_Size', 'VGPR_Count', 'Accum_VGPR_Count',
+                                         'SGPR_Count', 'Workgroup_Size_X', 'Grid_Size_X') if k in r}
+                break
+    except SystemExit:
+        pass
+    fetch_kib, nf = pmc_per_launch(os.path.join(a.raw, f'prof_{a.tag}_FETCH_SIZE'), 'FETCH_SIZE', kernel)
+    write_kib, nw = pmc_per_launch(os.path.join(a.raw, f'prof_{a.tag}_WRITE_SIZE'), 'WRITE_SIZE', kernel)
+    fetch, write = fetch_kib * 1024.0, write_kib * 1024.0
+    avg_ns = next(float(r['AverageNs']) for r in rows if short(r['Name']) == kernel)
+    pmc = {'tag': a.tag, 'kernel': kernel, 'resources': res,
+           'fetch_bytes_per_launch_raw': fetch, 'write_bytes_per_launch': write,
+           'fetch_bytes_per_launch_corrected': 2.0 * fetch,
+           'hbm_bytes_per_launch': 2.0 * fetch + write,
+           'hbm_bytes_per_launch_raw': fetch + write,
+           'dispatches': {'FETCH_SIZE': nf, 'WRITE_SIZE': nw}, 'avg_ns': avg_ns}
+    json.dump(pmc, open(os.path.join(a.dest, f'pmc_{kernel.split("<")[0]}.json'), 'w'), indent=1)
+    lines = [f'# rocprofv3 summary `{a.tag}` ({a.workload})', '',
+             f'Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py '
+             f'--workload {a.workload} --no-cpu-baseline --no-other --steps 200 --warmup 20`; '
+             f'PMC: `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`, separate runs, `--steps 30 --warmup 5` '
+             f'(tools/profile.sh).', '',
+             '| kernel | calls | avg us | min us | max us | % |', '|---|---|---|---|---|---|']
     for r in rows:
-        if kname in short_name(r['Name']):
-            out['avg_ns'] = float(r['AverageNs'])
-    json.dump(out, open(os.path.join(dst, f'pmc_{kname}.json'), 'w'), indent=1)
-    open(os.path.join(dst, f'{tag}_summary.md'), 'w').write('\n'.join(lines) + '\n')
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                     f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} | "
+                     f"{float(r['Percentage']):.1f} |")
+    lines += ['', f'{kernel} resources: `{res}`', '',
+              f'PMC per {kernel} launch: FETCH_SIZE {fetch / 1e6:.2f} MB raw '
+              f'(x2 gfx950 correction: {2 * fetch / 1e6:.2f} MB), WRITE_SIZE {write / 1e6:.2f} MB; '
+              f'HBM traffic {pmc["hbm_bytes_per_launch"] / 1e6:.2f} MB corrected '
+              f'({pmc["hbm_bytes_per_launch_raw"] / 1e6:.2f} MB raw).']
+    open(os.path.join(a.dest, base + '_summary.md'), 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
 
