@@ -1660,6 +1660,13 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
         const bool maybe = att && L.active && attack_precheck(p, sm, L);
         const uint64_t maybe_mask = __ballot(maybe);
+        // the launch lasts as long as its slowest env: an env with a long
+        // serial attack chain gets issue priority over the SIMD's other waves
+        {
+            const int nser = __popcll(maybe_mask);
+            if (nser >= 16) __builtin_amdgcn_s_setprio(2);
+            else if (nser >= 8) __builtin_amdgcn_s_setprio(1);
+        }
         for (uint64_t it = __ballot(att); it; it &= it - 1) {
             const int a = first_lane(it);
             if (!rlb(L.active, a)) continue;                // killed earlier this pass

@@ -83,3 +83,57 @@ def test_shard_invariance_with_oracle(oracle_mod):
         for k in range(4):
             joined = np.concatenate([halves[0][t][k], halves[1][t][k]])
             assert (joined == full[t][k]).all()
+
+
+def _rtt_rollout(oracle_mod, first, n, T=12, horizon=6, total=4):
+    """BASELINE config 4 (ReachTheTarget 64x64, 256 entities) on the oracle for
+    envs [first, first + n): per-env acting agent-steps and the final obs."""
+    from tests.cases import build_rtt, RTT_CONFIG4
+    cc = build_rtt(dict(RTT_CONFIG4)).compiled()
+    o = oracle_mod.Oracle(cc, n)
+    o.seed(env_seeds(n, run=6, first_env=first))
+    obs = o.new_obs()
+    o.reset(obs)
+    A = cc.n_agents
+    rng = np.random.RandomState(11)
+    acts = np.zeros((T, total, A, cc.act_dim), np.int32)         # per global env id
+    acts[..., :2] = rng.randint(-2, 3, size=(T, total, A, 2))
+    acts[..., 2:] = rng.randint(0, 2, size=(T, total, A, cc.act_dim - 2))
+    rew, done, ad = np.zeros((n, A)), np.zeros((n, A), np.uint8), np.zeros(n, np.uint8)
+    acting = np.zeros(n, np.uint64)
+    for t in range(T):
+        o.step(acts[t, first:first + n], obs, rew, done, ad, acting)
+        err = (o.errors() & 4) != 0
+        rs = (ad != 0) | err | (o.state()['steps'] >= horizon)
+        if rs.any():
+            o.reset(obs, mask=rs.astype(np.uint8))
+    return acting.astype(np.int64), obs.copy()
+
+
+def _rtt_worker(rank, world, port, out):
+    from oracle import oracle as oracle_mod
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    first, n = shard_envs(4, rank, world)
+    acting, obs = _rtt_rollout(oracle_mod, first, n)
+    s = gather_episode_stats(torch.as_tensor(acting), torch.zeros(n, dtype=torch.int32), dist)
+    out[rank] = (s, acting.tolist(), int(obs.astype(np.int64).sum()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config4_sharded_gloo(oracle_mod):
+    """Config 4 sharded over 2 gloo ranks (as over GPUs): each rank steps its
+    envs from their global seeds; the all-gathered episode stats equal one
+    rank running all envs, and the per-env results are the same."""
+    ref_acting, ref_obs = _rtt_rollout(oracle_mod, 0, 4)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29700 + (os.getpid() % 1000)
+    mp.spawn(_rtt_worker, args=(2, port, out), nprocs=2, join=True)
+    for r in range(2):
+        s = out[r][0]
+        assert s['envs'] == 4
+        assert s['acting_agent_steps_total'] == float(ref_acting.sum())
+    assert out[0][1] + out[1][1] == ref_acting.tolist()
+    assert out[0][2] + out[1][2] == int(ref_obs.astype(np.int64).sum())

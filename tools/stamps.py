@@ -41,6 +41,12 @@ def report(st, order, names, title):
         prev = i
 
 
+# one-wave-per-env kernel (gw_engine.hip step_kernel, STAMP indices)
+TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 2: 'attack pass', 3: 'move pass', 4: '-',
+           8: 'obs windows', 9: 'crowded draws', 5: 'obs store', 6: 'dones+store'}
+TB_NEXT = {0: 'start', 10: 'prologue', 12: '-', 13: 'placement+health', 14: 'tables+obs', 6: 'store'}
+
+
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else 'rtt'
     E = int(sys.argv[2]) if len(sys.argv) > 2 else (1024 if wl == 'rtt' else 4096)
@@ -52,7 +58,7 @@ def main():
     torch.cuda.synchronize()
     st = eng.stamps.cpu().numpy()
     report(st, [12, 17, 13, 14, 15, 16], RESET, f'{wl}: reset launch ({E} envs)')
-    if (st[:, 20] != 0).any():
+    if wl == 'rtt' and (st[:, 20] != 0).any():
         report(st, [17, 18, 19, 20], PLACE, 'parallel placement')
         sw = st[:, 21]
         print(f'{"sweeps":>24}: median {np.median(sw):.0f} max {sw.max()}')
@@ -63,9 +69,18 @@ def main():
         eng.step_autoreset_next(horizon=200)
     torch.cuda.synchronize()
     st = eng.stamps.cpu().numpy()
-    report(st, list(range(10)), STEP, f'{wl}: step launch 30 (next_step auto-reset)')
-    tot = st[:, 9] - st[:, 0]
-    print(f'whole step: median {np.median(tot):.0f} max {tot.max():.0f} ticks')
+    if wl == 'rtt':
+        report(st, list(range(10)), STEP, f'{wl}: step launch 30 (next_step auto-reset)')
+        tot = st[:, 9] - st[:, 0]
+    else:
+        stepped = st[:, 2] != 0
+        report(st[stepped], [0, 10, 1, 2, 3, 4, 8, 9, 5, 6], TB_STEP,
+               f'{wl}: step launch 30, stepping envs ({stepped.sum()})')
+        if (~stepped).any():
+            report(st[~stepped], [0, 10, 12, 13, 14, 6], TB_NEXT, f'{wl}: resetting envs ({(~stepped).sum()})')
+        tot = st[:, 6] - st[:, 0]
+    print(f'whole launch per env: median {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f} '
+          f'max {tot.max():.0f} ticks')
 
 
 if __name__ == '__main__':
