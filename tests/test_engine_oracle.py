@@ -56,6 +56,19 @@ def test_headline_config_4096_envs(oracle_mod):
 
 
 @pytest.mark.parametrize('kw', [
+    # accuracy < 1, crowded, 3 teams
+    dict(rows=8, cols=8, n_agents=40, n_teams=3,
+         agent=dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=0.6, view_range=2)),
+    # attack range 2: up to 25 window cells
+    dict(rows=10, cols=10, n_agents=48, n_teams=2,
+         agent=dict(move_range=1, attack_range=2, attack_strength=1, attack_accuracy=0.9, view_range=3)),
+])
+def test_dense_attack_configs(oracle_mod, kw):
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=1024, T=100, horizon=40, seed_run=8, key=21, check_every=2)
+
+
+@pytest.mark.parametrize('kw', [
     dict(rows=8, cols=8, n_agents=16, n_teams=2),
     dict(rows=5, cols=5, n_agents=20, n_teams=4),
     dict(rows=12, cols=20, n_agents=64, n_teams=3,
