@@ -65,6 +65,7 @@ namespace {
 struct DevAgent {               // per-entity constants (spec table in HBM)
     int32_t enc;
     uint32_t kind;
+    uint32_t ov, amap;          // overlap / attack-mapping masks of enc (no dependent load)
     int32_t init_r, init_c;
     int32_t view_range, move_range, attack_range, simul;
     double strength, accuracy, init_health;
@@ -373,28 +374,28 @@ struct Lane {
 
 __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool valid)
 {
+    // unconditional loads (lanes past A read lane 0's row), then selects: a
+    // branch around the loads would make its join wait for them
     const int l = lane_id();
-    if (valid) {
-        const DevAgent s = p.spec[l];
-        L.enc = s.enc; L.kind = s.kind; L.view = s.view_range; L.mrange = s.move_range;
-        L.arange = s.attack_range; L.simul = s.simul; L.strength = s.strength;
-        L.accuracy = s.accuracy; L.init_health = s.init_health; L.init_r = s.init_r;
-        L.init_c = s.init_c;
-        L.ov = p.overlap[s.enc];
-        L.amap = p.amap[s.enc];
-        size_t k = (size_t)e * p.A + l;
-        int2 q = p.pos[k];
-        L.r = q.x; L.c = q.y;
-        L.seq = p.seq[k];
-        L.health = p.health[k];
-        uint8_t f = p.flags[k];
-        L.in_grid = f & F_IN_GRID; L.live = f & F_LIVE; L.active = f & F_ACTIVE;
-    } else {
-        L.enc = 0; L.kind = 0; L.view = L.mrange = L.arange = L.simul = 0;
-        L.strength = L.accuracy = L.init_health = 0; L.init_r = L.init_c = -1; L.ov = 0;
-        L.amap = 0;
-        L.r = L.c = -1000; L.seq = 0; L.health = 0; L.in_grid = L.live = L.active = false;
-    }
+    const int li = valid ? l : 0;
+    const DevAgent s = p.spec[li];
+    const size_t k = (size_t)e * p.A + li;
+    const int2 q = p.pos[k];
+    const uint32_t sq = p.seq[k];
+    const double h = p.health[k];
+    const uint8_t f = p.flags[k];
+    L.enc = valid ? s.enc : 0; L.kind = valid ? s.kind : 0u;
+    L.view = valid ? s.view_range : 0; L.mrange = valid ? s.move_range : 0;
+    L.arange = valid ? s.attack_range : 0; L.simul = valid ? s.simul : 0;
+    L.strength = valid ? s.strength : 0.0; L.accuracy = valid ? s.accuracy : 0.0;
+    L.init_health = valid ? s.init_health : 0.0;
+    L.init_r = valid ? s.init_r : -1; L.init_c = valid ? s.init_c : -1;
+    L.ov = valid ? s.ov : 0u;
+    L.amap = valid ? s.amap : 0u;
+    L.r = valid ? q.x : -1000; L.c = valid ? q.y : -1000;
+    L.seq = valid ? sq : 0u;
+    L.health = valid ? h : 0.0;
+    L.in_grid = valid && (f & F_IN_GRID); L.live = valid && (f & F_LIVE); L.active = valid && (f & F_ACTIVE);
     L.reward = 0.0;
 }
 
@@ -1609,22 +1610,26 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     const bool valid = l < A;
     STAMP(0);
     Smem sm = carve(smem_raw, p);
-    // epilogue counters read up front (not a dependent load at the end)
-    const int32_t steps0 = uni(p.steps[e]);
-    const bool next_reset = p.autoreset == 2 &&
-                            (uni((uint32_t)p.all_done[e]) != 0u || (p.horizon > 0 && steps0 >= p.horizon));
+    // every global load of the prologue is issued before any is used (one
+    // memory round trip): the epilogue counters, the previous __all__ (read
+    // unconditionally: a branch on it would wait for it), lanes, actions
+    const int32_t steps_raw = p.steps[e];
+    const uint32_t ad_raw = p.all_done[e];
     Lane L;
     load_lane(p, e, L, valid);
     // actions (lane = agent); attack == -1 marks "not in action_dict"
-    int mr = 0, mc = 0, ak = -1;
-    if (valid) {
-        const int32_t* ap = p.actions + ((size_t)e * A + l) * p.act_dim;
-        mr = ap[0]; mc = ap[1]; ak = ap[2];
+    int mr, mc, ak;
+    {
+        const int32_t* ap = p.actions + ((size_t)e * A + (valid ? l : 0)) * p.act_dim;
+        const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
+        mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
     }
     const uint64_t acting0 = p.acting ? p.acting[e] : 0ull;
     Rng rng;
     uint32_t ctr;
     load_env(p, e, sm, rng, ctr, true);
+    const int32_t steps0 = uni(steps_raw);
+    const bool next_reset = p.autoreset == 2 && (uni(ad_raw) != 0u || (p.horizon > 0 && steps0 >= p.horizon));
     if (next_reset) {
         // NEXT_STEP auto-reset: the episode ended in the previous call, so
         // this call is AllStepManager.reset for the env (actions ignored):
@@ -2363,6 +2368,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int l = 0; l < A; l++) {
         const gw_agent_spec& s = cfg->agents[lanes[l]];
         hs[l].enc = s.encoding; hs[l].kind = s.kind; hs[l].init_r = s.init_row; hs[l].init_c = s.init_col;
+        hs[l].ov = cfg->overlap[s.encoding]; hs[l].amap = cfg->attack_mapping[s.encoding];
         hs[l].view_range = s.view_range; hs[l].move_range = s.move_range;
         hs[l].attack_range = s.attack_range; hs[l].simul = s.simultaneous_attacks;
         hs[l].strength = s.attack_strength; hs[l].accuracy = s.attack_accuracy;
