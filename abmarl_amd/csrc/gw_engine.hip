@@ -348,6 +348,18 @@ struct Rng {
         return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
     }
 
+    // n words consumed without looking at them (draws whose outcome is fixed:
+    // uniform() > accuracy never holds for accuracy >= 1)
+    __device__ __forceinline__ void skip(int n)
+    {
+        while (n > 0) {
+            if (pos == GW_MT_N) twist();
+            const int s = n < GW_MT_N - pos ? n : GW_MT_N - pos;
+            pos += s;
+            n -= s;
+        }
+    }
+
     // masked rejection draw on [0, max]; zero draws when max == 0
     __device__ __forceinline__ uint32_t interval(uint32_t max)
     {
@@ -884,6 +896,28 @@ __device__ __forceinline__ bool attack_precheck(const Params& p, const Smem& sm,
 {
     const int R = L.arange;
     bool any = false;
+    if (R == 1) {
+        // three window rows, one aligned dword each (independent LDS reads)
+        const uint32_t* t32 = (const uint32_t*)sm.tbl;
+        const int o0 = tbl_idx(p, L.r - 1, L.c - 1);
+        uint32_t w[3];
+#pragma unroll
+        for (int wr = 0; wr < 3; wr++) {
+            const int o = o0 + wr * p.pitch;
+            w[wr] = __builtin_amdgcn_alignbyte(t32[(o >> 2) + 1], t32[o >> 2], o & 3);
+        }
+#pragma unroll
+        for (int wr = 0; wr < 3; wr++) {
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                const uint32_t v = (w[wr] >> (8 * b)) & 0xffu;
+                if (v == CELL_OFF || v == 0) continue;
+                if (wr == 1 && b == 1 && v != CELL_CROWD) continue;    // just me
+                if (v == CELL_CROWD || ((L.amap >> (v & 31u)) & 1u)) any = true;
+            }
+        }
+        return any;
+    }
     for (int dr = -R; dr <= R; dr++) {
         for (int dc = -R; dc <= R; dc++) {
             const uint32_t b = sm.tbl[tbl_idx(p, L.r + dr, L.c + dc)];
@@ -946,14 +980,21 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     const int ncand = __popcll(cm);
     int rank = -1;                                         // rank among accepted
     int n = 0;
-    for (int r = 0; r < ncand; r++) {
-        const uint64_t jm = __ballot(crank == r);
-        CHECK(__popcll(jm) == 1, 8, r, ncand);
-        const int j = first_lane(jm);
-        const double u = rng.uniform();                     // _basic_criteria draw
-        if (u > acc) continue;
-        if (l == j) rank = n;
-        n++;
+    if (acc >= 1.0) {
+        // uniform() is < 1: every candidate passes its accuracy draw
+        rng.skip(2 * ncand);
+        rank = crank;
+        n = ncand;
+    } else {
+        for (int r = 0; r < ncand; r++) {
+            const uint64_t jm = __ballot(crank == r);
+            CHECK(__popcll(jm) == 1, 8, r, ncand);
+            const int j = first_lane(jm);
+            const double u = rng.uniform();                 // _basic_criteria draw
+            if (u > acc) continue;
+            if (l == j) rank = n;
+            n++;
+        }
     }
     if (n == 0) return true;                                // (True, [])
     // _subset_attackables: pick (lane t) = accepted rank of list[t]
@@ -1060,6 +1101,18 @@ __device__ __forceinline__ bool attack_selective(const Params& p, Smem& sm, Rng&
         // _basic_criteria in cell (seq) order: accuracy draws
         int arank = -1;                                     // rank among this cell's accepted
         int n = 0;
+        if (acc >= 1.0) {                                   // every draw passes: ranks by seq
+            const int nm = __popcll(mm);
+            rng.skip(2 * nm);
+            int rk = 0;
+            for (uint64_t it = mm; it; it &= it - 1) {
+                const uint32_t sqm = rl(L.seq, first_lane(it));
+                rk += (here && sqm < L.seq) ? 1 : 0;
+            }
+            if (here) arank = rk;
+            n = nm;
+            mm = 0;
+        }
         while (mm) {
             uint32_t best = 0xFFFFFFFFu;
             int j = -1;
@@ -1671,14 +1724,28 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
             const int nser = __popcll(maybe_mask);
             if (nser >= 16) __builtin_amdgcn_s_setprio(2);
             else if (nser >= 8) __builtin_amdgcn_s_setprio(1);
-        }
-        for (uint64_t it = __ballot(att); it; it &= it - 1) {
-            const int a = first_lane(it);
-            if (!rlb(L.active, a)) continue;                // killed earlier this pass
-            if (!((maybe_mask >> a) & 1)) {                  // no possible target: (True, [])
-                if (l == a) L.reward -= 0.1;
-                continue;
+#ifdef GW_STAMPS
+            const int natt = __popcll(__ballot(att));
+            if (l == 0 && p.stamps) {
+                p.stamps[(size_t)e * 32 + 28] = nser;
+                p.stamps[(size_t)e * 32 + 29] = natt;
             }
+#endif
+        }
+        STAMP(7);
+        // Only attackers with a possible target run serially.  The others get
+        // (True, []) -> -0.1 if still active at their turn: applied lane-parallel
+        // just before the next serial attacker after them (so each lane's
+        // reward terms keep their reference order), or after the loop.
+        uint64_t pend = __ballot(att) & ~maybe_mask;
+        for (uint64_t it = maybe_mask; it; it &= it - 1) {
+            const int a = first_lane(it);
+            const uint64_t before = pend & ((1ull << a) - 1ull);
+            if (before) {
+                if (((before >> l) & 1ull) && L.active) L.reward -= 0.1;
+                pend &= ~before;
+            }
+            if (!rlb(L.active, a)) continue;                // killed earlier this pass
             int nlist, list;
             attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
             if (nlist == 0) { if (l == a) L.reward -= 0.1; }
@@ -1692,6 +1759,7 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
                 }
             }
         }
+        if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
         STAMP(2);
         // ---- move pass (:50-55)
         const bool mover = acting && L.active;

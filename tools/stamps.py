@@ -42,7 +42,7 @@ def report(st, order, names, title):
 
 
 # one-wave-per-env kernel (gw_engine.hip step_kernel, STAMP indices)
-TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 2: 'attack pass', 3: 'move pass', 4: '-',
+TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 7: 'attack precheck', 2: 'attack loop', 3: 'move pass', 4: '-',
            8: 'obs windows', 9: 'crowded draws', 5: 'obs store', 6: 'dones+store'}
 TB_NEXT = {0: 'start', 10: 'prologue', 12: '-', 13: 'placement+health', 14: 'tables+obs', 6: 'store'}
 
@@ -74,11 +74,22 @@ def main():
         tot = st[:, 9] - st[:, 0]
     else:
         stepped = st[:, 2] != 0
-        report(st[stepped], [0, 10, 1, 2, 3, 4, 8, 9, 5, 6], TB_STEP,
+        report(st[stepped], [0, 10, 1, 7, 2, 3, 4, 8, 9, 5, 6], TB_STEP,
                f'{wl}: step launch 30, stepping envs ({stepped.sum()})')
         if (~stepped).any():
             report(st[~stepped], [0, 10, 12, 13, 14, 6], TB_NEXT, f'{wl}: resetting envs ({(~stepped).sum()})')
         tot = st[:, 6] - st[:, 0]
+    if wl != 'rtt':
+        ns, na = st[:, 28], st[:, 29]
+        at = st[:, 2] - st[:, 1]
+        ok = ns > 0
+        print(f'attackers per env: median {np.median(na):.0f}, with a possible target {np.median(ns):.0f} '
+              f'(max {ns.max()}); attack ticks per such attacker: median {np.median(at[ok] / ns[ok]):.0f}')
+        for lo, hi in [(0, 4), (4, 8), (8, 16), (16, 64)]:
+            m = (ns >= lo) & (ns < hi)
+            if m.any():
+                print(f'   {lo:2d}-{hi:2d} possible-target attackers: {m.sum():5d} envs, attack pass median '
+                      f'{np.median(at[m]):.0f} ticks')
     print(f'whole launch per env: median {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f} '
           f'max {tot.max():.0f} ticks')
 
