@@ -1789,6 +1789,13 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
         bool moved = false;
         if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)l; moved = true; }
         bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
+#ifdef GW_STAMPS
+        {
+            const int nser = __popcll(__ballot(real && !iso)), nreal = __popcll(__ballot(real));
+            if (l == 0 && p.stamps) { p.stamps[(size_t)e * 32 + 30] = nser; p.stamps[(size_t)e * 32 + 31] = nreal; }
+        }
+#endif
+        STAMP(11);
         for (uint64_t it = __ballot(real && !iso); it; it &= it - 1) {
             const int a = first_lane(it);
             const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);

@@ -42,7 +42,8 @@ def report(st, order, names, title):
 
 
 # one-wave-per-env kernel (gw_engine.hip step_kernel, STAMP indices)
-TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 7: 'attack precheck', 2: 'attack loop', 3: 'move pass', 4: '-',
+TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 7: 'attack precheck', 2: 'attack loop',
+           11: 'move isolation', 3: 'serial moves+table', 4: '-',
            8: 'obs windows', 9: 'crowded draws', 5: 'obs store', 6: 'dones+store'}
 TB_NEXT = {0: 'start', 10: 'prologue', 12: '-', 13: 'placement+health', 14: 'tables+obs', 6: 'store'}
 
@@ -74,7 +75,7 @@ def main():
         tot = st[:, 9] - st[:, 0]
     else:
         stepped = st[:, 2] != 0
-        report(st[stepped], [0, 10, 1, 7, 2, 3, 4, 8, 9, 5, 6], TB_STEP,
+        report(st[stepped], [0, 10, 1, 7, 2, 11, 3, 4, 8, 9, 5, 6], TB_STEP,
                f'{wl}: step launch 30, stepping envs ({stepped.sum()})')
         if (~stepped).any():
             report(st[~stepped], [0, 10, 12, 13, 14, 6], TB_NEXT, f'{wl}: resetting envs ({(~stepped).sum()})')
@@ -85,6 +86,8 @@ def main():
         ok = ns > 0
         print(f'attackers per env: median {np.median(na):.0f}, with a possible target {np.median(ns):.0f} '
               f'(max {ns.max()}); attack ticks per such attacker: median {np.median(at[ok] / ns[ok]):.0f}')
+        print(f'movers per env: median {np.median(st[:, 31]):.0f}, not isolated (serial) median '
+              f'{np.median(st[:, 30]):.0f} max {st[:, 30].max()}')
         for lo, hi in [(0, 4), (4, 8), (8, 16), (16, 64)]:
             m = (ns >= lo) & (ns < hi)
             if m.any():
