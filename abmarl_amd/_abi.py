@@ -58,6 +58,7 @@ GW_ORDER_HEALTH_POSITION = 1
 FLAG_IN_GRID = 1
 FLAG_LIVE = 2
 FLAG_ACTIVE = 4
+FLAG_OBS_M2 = 0x40   # engine-internal (gw_config.persistent_obs): the lane's obs row holds -2
 
 
 class AgentSpec(C.Structure):
@@ -99,6 +100,8 @@ class Config(C.Structure):
         ("pacman_agent", C.c_int32),
         ("tunnel", C.c_int32 * 4),
         ("pac_rewards", C.c_double * 5),
+        ("force_workgroup", C.c_int32),
+        ("persistent_obs", C.c_int32),
     ]
 
 
@@ -110,7 +113,7 @@ class CompiledConfig:
                  state_order=GW_ORDER_POSITION_HEALTH, done_kind=GW_DONE_ACTIVE,
                  obs_range=0, target_agent=-1, nav_agent=-1, attack_kind=0,
                  obs_kind=GW_OBS_POSITION_CENTERED, pacman_agent=-1, tunnel=(-1, -1, -1, -1),
-                 pac_rewards=(0.0, 0.0, 0.0, 0.0, 0.0)):
+                 pac_rewards=(0.0, 0.0, 0.0, 0.0, 0.0), force_workgroup=False):
         self.n_agents = len(specs)
         self._specs = (AgentSpec * max(1, self.n_agents))()
         for i, s in enumerate(specs):
@@ -136,6 +139,7 @@ class CompiledConfig:
             cfg.tunnel[i] = int(tunnel[i])
         for i in range(5):
             cfg.pac_rewards[i] = float(pac_rewards[i])
+        cfg.force_workgroup = int(bool(force_workgroup))
         self.cfg = cfg
         self.rows, self.cols = rows, cols
         self.obs_kind = obs_kind

@@ -38,6 +38,8 @@ SIGNATURES = {
     'gw_get_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_set_state': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_random_actions': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp]),
+    'gw_rollout_step': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+                               _vp, _vp]),
     'gw_destroy': (_i32, [_vp]),
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),
@@ -59,22 +61,50 @@ SIGNATURES = {
 }
 
 
+PART_SIDES = (1, 3, 5, 7, 9, 11, 13, 15)   # observation window sides S = 2*range+1
+
+
 def build(force=False, verbose=False, stamps=False, checks=False):
-    """Compile the engine for gfx950 with hipcc (works without a GPU)."""
+    """Compile the engine for gfx950 with hipcc (works without a GPU).
+
+    gw_engine.hip is compiled as one host part plus one part per window side
+    S (-DGW_PART_S, the templated step/reset kernels), in parallel, then
+    linked into one shared library."""
     out = LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB)
-    deps = [SRC, INCLUDE, os.path.join(os.path.dirname(SRC), 'gw_pacman.inc'),
-            os.path.join(os.path.dirname(SRC), 'gw_rtt.inc')]
+    csrc = os.path.dirname(SRC)
+    deps = [SRC, INCLUDE] + [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith('.inc')]
     if not force and os.path.exists(out) and \
             os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off',
-           '-fPIC', '-shared', '-Wno-unused-result'] + (['-DGW_STAMPS'] if stamps else []) + \
-        (['-DGW_CHECKS'] if checks else []) + \
-        ['-o', out + '.tmp', SRC]
+    tag = 'stamps' if stamps else ('checks' if checks else 'prod')
+    flags = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off', '-fPIC',
+             '-Wno-unused-result'] + (['-DGW_STAMPS'] if stamps else []) + \
+        (['-DGW_CHECKS'] if checks else [])
+    objdir = os.path.join(os.path.dirname(out), f'obj_{tag}')
+    os.makedirs(objdir, exist_ok=True)
+    jobs = [(os.path.join(objdir, 'host.o'), [])] + \
+        [(os.path.join(objdir, f'part_s{s}.o'), [f'-DGW_PART_S={s}']) for s in PART_SIDES]
+    cmds = [[HIPCC] + flags + extra + ['-c', '-o', o, SRC] for o, extra in jobs]
     if verbose:
-        print(' '.join(cmd))
-    subprocess.check_call(cmd)
+        for c in cmds:
+            print(' '.join(c))
+    par = max(1, min(len(cmds), int(os.environ.get('MAX_JOBS', '0')) or (os.cpu_count() or 1)))
+    running, failed = [], []
+    pending = list(cmds)
+    while pending or running:
+        while pending and len(running) < par:
+            c = pending.pop(0)
+            running.append((c, subprocess.Popen(c)))
+        c, pr = running.pop(0)
+        if pr.wait() != 0:
+            failed.append(' '.join(c))
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', out + '.tmp'] + [o for o, _ in jobs]
+    if verbose:
+        print(' '.join(link))
+    subprocess.check_call(link)
     os.replace(out + '.tmp', out)
     return out
 

@@ -51,6 +51,7 @@
 #define F_IN_GRID 1u
 #define F_LIVE 2u
 #define F_ACTIVE 4u
+#define F_OBS_M2 0x40u      // persistent obs buffer: this lane's row holds -2 (engine-internal)
 #define MT_POS_SLOT 624
 #define MT_CTR_SLOT 625
 #define MT_CBASE_SLOT 626   // base of the cached tempered block (0xFFFFFFFF: none)
@@ -128,6 +129,7 @@ struct Params {
     int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
     int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
+    int32_t persistent_obs;                // gw_config.persistent_obs: skip rows already -2
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -381,6 +383,7 @@ struct Lane {
     int init_r, init_c;
     // state
     int r, c; uint32_t seq; double health; bool in_grid, live, active;
+    bool obs_m2;         // F_OBS_M2: the persistent obs row already holds -2
     double reward;
 };
 
@@ -408,6 +411,7 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
     L.seq = valid ? sq : 0u;
     L.health = valid ? h : 0.0;
     L.in_grid = valid && (f & F_IN_GRID); L.live = valid && (f & F_LIVE); L.active = valid && (f & F_ACTIVE);
+    L.obs_m2 = valid && (f & F_OBS_M2);
     L.reward = 0.0;
 }
 
@@ -419,7 +423,8 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
     p.pos[k] = make_int2(L.r, L.c);
     p.seq[k] = L.seq;
     p.health[k] = L.health;
-    p.flags[k] = (uint8_t)((L.in_grid ? F_IN_GRID : 0) | (L.live ? F_LIVE : 0) | (L.active ? F_ACTIVE : 0));
+    p.flags[k] = (uint8_t)((L.in_grid ? F_IN_GRID : 0) | (L.live ? F_LIVE : 0) | (L.active ? F_ACTIVE : 0) |
+                           (L.obs_m2 ? F_OBS_M2 : 0));
 }
 
 // LDS carve-up per wave (dynamic shared memory, 16-B aligned pieces)
@@ -605,7 +610,7 @@ __host__ __device__ constexpr int stage_pitch(int S) { return (S + 3) & ~3; }
 
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S>
-__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, const Lane& L,
+__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
                                             int stamp_base = 8)
 {
     (void)stamp_base;
@@ -618,6 +623,10 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     const int l = lane_id();
     const int A = p.A;
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
+    // persistent obs buffer (gw_config.persistent_obs): rows that already
+    // hold -2 and stay -2 (done entities, non-observers) are not rewritten
+    const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me) : 0ull;
+    if (l < A) L.obs_m2 = !obs_me;
 
     // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
     // static blockers precomputed per cell, blocking lanes from the shadow LUT
@@ -874,7 +883,10 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
 #pragma unroll
             for (int k = 0; k < B; k++) {
                 const int m = ((k0 + k) * WAVE + l) * 4;
-                if (m < total) {
+                // the four outputs belong to lanes m / SS and (m + 3) / SS
+                const bool keep = m < total &&
+                                  !((skip >> (m / SS)) & (skip >> ((m + 3) / SS)) & 1ull);
+                if (keep) {
                     const uint32_t w = __builtin_amdgcn_perm(hi[k], lo[k], sel[k]);
                     *(int4*)(out + m) = make_int4((int8_t)(w & 0xff), (int8_t)((w >> 8) & 0xff),
                                                   (int8_t)((w >> 16) & 0xff), (int8_t)(w >> 24));
@@ -884,7 +896,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     } else {
         for (int m = l; m < total; m += WAVE) {
             const int q = m / S;
-            out[m] = sm.stage[m + q * (SP - S)];
+            if (!((skip >> (m / SS)) & 1ull)) out[m] = sm.stage[m + q * (SP - S)];
         }
     }
 }
@@ -1996,6 +2008,7 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
     uint32_t ctr;
     load_env(p, e, sm, rng, ctr, false);
     ctr = 0;
+    if (l == 0 && p.err) p.err[e] = 0u;     // an explicit reset starts the env's flags afresh
     reset_env<S>(p, e, sm, rng, L, ctr, false);
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
@@ -2093,10 +2106,57 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
     }
 }
 
+#ifndef GW_PART_S
 #include "gw_pacman.inc"
+#endif
 #include "gw_rtt.inc"
 
 }  // namespace
+
+// ====================================================== per-window-size parts
+// The templated kernels are instantiated once per observation window side S
+// in their own translation unit (-DGW_PART_S=<S>; _native.build compiles the
+// parts in parallel and links them with the host part).  Each part exports a
+// launcher and an attribute setter; the host part dispatches on S to them.
+enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3 };
+typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
+                                     hipStream_t st, const void* params);
+typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
+#define GW_PART_CAT2(a, b) a##b
+#define GW_PART_CAT(a, b) GW_PART_CAT2(a, b)
+#define GW_PART_DECL(S_)                                                                      \
+    hipError_t GW_PART_CAT(gw_part_launch_, S_)(int, unsigned, unsigned, size_t, hipStream_t, \
+                                                const void*);                                 \
+    hipError_t GW_PART_CAT(gw_part_attr_, S_)(int, size_t);
+GW_PART_DECL(1) GW_PART_DECL(3) GW_PART_DECL(5) GW_PART_DECL(7)
+GW_PART_DECL(9) GW_PART_DECL(11) GW_PART_DECL(13) GW_PART_DECL(15)
+
+#ifdef GW_PART_S
+hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsigned block, size_t smem,
+                                                   hipStream_t st, const void* params)
+{
+    const Params& p = *static_cast<const Params*>(params);
+    constexpr int S = GW_PART_S;
+    switch (kind) {
+    case PK_STEP: hipLaunchKernelGGL(step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_RESET: hipLaunchKernelGGL(reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_WG_STEP: hipLaunchKernelGGL(wg_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
+{
+    constexpr int S = GW_PART_S;
+    const void* k = kind == PK_STEP ? (const void*)step_kernel<S>
+                  : kind == PK_RESET ? (const void*)reset_kernel<S>
+                  : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
+                                       : (const void*)wg_reset_kernel<S>;
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+#else   // ------------------------------------------------------- host part
 
 // ====================================================================== C-ABI
 struct gw_engine {
@@ -2177,68 +2237,26 @@ static void set_err(const char* fmt, ...)
         }                                                                         \
     } while (0)
 
-template <int S>
-static hipError_t launch_step(const gw_engine* g, const Params& p, hipStream_t st)
+// the parts, indexed by S / 2 (S = 1, 3, ..., 15)
+static const part_launch_fn k_part_launch[8] = {
+    gw_part_launch_1, gw_part_launch_3, gw_part_launch_5, gw_part_launch_7,
+    gw_part_launch_9, gw_part_launch_11, gw_part_launch_13, gw_part_launch_15};
+static const part_attr_fn k_part_attr[8] = {
+    gw_part_attr_1, gw_part_attr_3, gw_part_attr_5, gw_part_attr_7,
+    gw_part_attr_9, gw_part_attr_11, gw_part_attr_13, gw_part_attr_15};
+
+static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const Params& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(step_kernel<S>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
-    return hipGetLastError();
+    if (g->S < 1 || g->S > 15 || !(g->S & 1)) return hipErrorInvalidValue;
+    const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET) ? WAVE * p.nwv : WAVE;
+    return k_part_launch[g->S >> 1](kind, (unsigned)g->E, block, smem, st, &p);
 }
 
-template <int S>
-static hipError_t launch_reset(const gw_engine* g, const Params& p, hipStream_t st)
+static hipError_t set_part_attrs(int S, int k0, int k1, size_t a, size_t b)
 {
-    hipLaunchKernelGGL(reset_kernel<S>, dim3(g->E), dim3(WAVE), g->smem_reset, st, p);
-    return hipGetLastError();
-}
-
-#ifdef GW_ONLY_S   /* diagnostic builds: one window size */
-#define DISPATCH_S(S_, FN, ...)                      \
-    switch (S_) {                                    \
-    case GW_ONLY_S: return FN<GW_ONLY_S>(__VA_ARGS__); \
-    default: return hipErrorInvalidValue;            \
-    }
-#else
-#define DISPATCH_S(S_, FN, ...)                      \
-    switch (S_) {                                    \
-    case 1: return FN<1>(__VA_ARGS__);               \
-    case 3: return FN<3>(__VA_ARGS__);               \
-    case 5: return FN<5>(__VA_ARGS__);               \
-    case 7: return FN<7>(__VA_ARGS__);               \
-    case 9: return FN<9>(__VA_ARGS__);               \
-    case 11: return FN<11>(__VA_ARGS__);             \
-    case 13: return FN<13>(__VA_ARGS__);             \
-    case 15: return FN<15>(__VA_ARGS__);             \
-    default: return hipErrorInvalidValue;            \
-    }
-#endif
-
-template <int S>
-static hipError_t launch_wg_step(const gw_engine* g, const Params& p, hipStream_t st)
-{
-    hipLaunchKernelGGL(wg_step_kernel<S>, dim3(g->E), dim3(WAVE * p.nwv), g->smem_step, st, p);
-    return hipGetLastError();
-}
-
-template <int S>
-static hipError_t launch_wg_reset(const gw_engine* g, const Params& p, hipStream_t st)
-{
-    hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(g->E), dim3(WAVE * p.nwv), g->smem_reset, st, p);
-    return hipGetLastError();
-}
-
-template <int S>
-static hipError_t set_wg_attr(size_t b)
-{
-    hipError_t e = hipFuncSetAttribute((const void*)wg_step_kernel<S>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)wg_reset_kernel<S>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
-}
-
-static hipError_t set_wg_attrs(int S, size_t b)
-{
-    DISPATCH_S(S, set_wg_attr, b);
+    if (S < 1 || S > 15 || !(S & 1)) return hipErrorInvalidValue;
+    hipError_t e = k_part_attr[S >> 1](k0, a);
+    return e != hipSuccess ? e : k_part_attr[S >> 1](k1, b);
 }
 
 static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st)
@@ -2250,30 +2268,13 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
-    if (g->wg) { DISPATCH_S(g->S, launch_wg_step, g, p, st); }
-    DISPATCH_S(g->S, launch_step, g, p, st);
+    return part_launch(g, g->wg ? PK_WG_STEP : PK_STEP, g->smem_step, p, st);
 }
 
 static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_RESET_ALL; return launch_pac(g, p, st); }
-    if (g->wg) { DISPATCH_S(g->S, launch_wg_reset, g, p, st); }
-    DISPATCH_S(g->S, launch_reset, g, p, st);
-}
-
-template <int S>
-static hipError_t set_smem_attr(size_t step_b, size_t reset_b)
-{
-    hipError_t e = hipFuncSetAttribute((const void*)step_kernel<S>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)step_b);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)reset_kernel<S>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)reset_b);
-}
-
-static hipError_t set_attrs(int S, size_t a, size_t b)
-{
-    DISPATCH_S(S, set_smem_attr, a, b);
+    return part_launch(g, g->wg ? PK_WG_RESET : PK_RESET, g->smem_reset, p, st);
 }
 
 extern "C" {
@@ -2382,11 +2383,14 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     const int A = (int)lanes.size();
     // ReachTheTarget runs on a workgroup per env when it has more lanes than a
-    // wave (or when GW_RTT_KERNEL=wg asks for it: the parity tests run the
-    // small reference fixtures through it)
-    const char* rk = getenv("GW_RTT_KERNEL");
+    // wave (or when the config forces it: the parity tests run the small
+    // reference fixtures through it)
+    if (cfg->force_workgroup && !(rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE)) {
+        set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor");
+        return GW_E_UNSUPPORTED;
+    }
     const bool wg = rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE &&
-                    (A > GW_MAX_AGENTS || (rk && strcmp(rk, "wg") == 0));
+                    (A > GW_MAX_AGENTS || cfg->force_workgroup);
     const int max_lanes = wg ? GW_MAX_LANES : GW_MAX_AGENTS;
     if (A == 0 || A > max_lanes) {
         set_err("%d dynamic entities outside 1..%d (%s)", A, max_lanes,
@@ -2466,6 +2470,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     p.act_dim = gw_config_act_dim(cfg);
     p.attack_kind = cfg->attack_kind;
+    p.persistent_obs = cfg->persistent_obs != 0;
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
@@ -2642,8 +2647,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
     HIPCHK(hipMemset(p.racc, 0, EA * sizeof(double)));
-    if (wg) HIPCHK(set_wg_attrs(g->S, g->smem_step));
-    else HIPCHK(set_attrs(g->S, g->smem_step, g->smem_reset));
+    if (wg) HIPCHK(set_part_attrs(g->S, PK_WG_STEP, PK_WG_RESET, g->smem_step, g->smem_step));
+    else HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
     *out = g;
     return GW_OK;
 }
@@ -2898,4 +2903,21 @@ gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t e
     return GW_OK;
 }
 
+gw_status gw_rollout_step(gw_handle g, uint64_t key, uint32_t step, uint32_t env_offset,
+                          int32_t* actions, int32_t* obs, double* reward, uint8_t* done,
+                          uint8_t* all_done, uint64_t* acting, int32_t horizon, int32_t autoreset,
+                          uint32_t* err_flags, void* stream)
+{
+    if (!g || !actions || !obs || !reward || !done || !all_done || autoreset < 0 || autoreset > 2)
+        return GW_E_INVALID;
+    const gw_status s = gw_random_actions(g, key, step, env_offset, actions, stream);
+    if (s != GW_OK) return s;
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
+    HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
 }  // extern "C"
+#endif  // GW_PART_S

@@ -39,8 +39,13 @@ class GridWorldEngine:
             self.device = torch.device('cuda', torch.cuda.current_device())
         self.E, self.S = int(n_envs), compiled.obs_side
         h = C.c_void_p()
+        # the engine passes its own obs buffer to every call: rows that hold
+        # -2 and stay -2 are not rewritten (gw_config.persistent_obs)
+        cfg = _abi.Config.from_buffer_copy(compiled.cfg)
+        cfg.persistent_obs = 1
+        self._cfg = cfg
         with torch.cuda.device(self.device):
-            _native.check(self.L.gw_create(C.cast(C.byref(compiled.cfg), C.c_void_p), self.E,
+            _native.check(self.L.gw_create(C.cast(C.byref(cfg), C.c_void_p), self.E,
                                            self.device.index, C.byref(h)), 'gw_create')
         self.h = h
         # per-env arrays are per lane; static entities (never move / act /
@@ -107,9 +112,9 @@ class GridWorldEngine:
             _native.check(self.L.gw_seed(self.h, _ptr(s), _stream()), 'gw_seed')
             torch.cuda.current_stream().synchronize()
 
-    def reset(self, mask=None, all_done=None, horizon=0, obs=None):
+    def reset(self, mask=None, all_done=None, horizon=0):
         """Reset selected envs (all of them by default); returns the obs buffer."""
-        out = self.obs if obs is None else obs
+        out = self.obs
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_reset(self.h, _ptr(mask), _ptr(all_done), int(horizon),
                                           _ptr(out), _ptr(self.err), _stream()), 'gw_reset')
@@ -234,6 +239,27 @@ class GridWorldEngine:
                                                    int(env_offset) & 0xFFFFFFFF, _ptr(out),
                                                    _stream()), 'gw_random_actions')
         return out
+
+    AUTORESET_MODES = {'none': 0, 'same_step': 1, 'next_step': 2}
+
+    def rollout_step(self, key, step, env_offset=0, horizon=0, autoreset='next_step'):
+        """One synthetic random-policy rollout step in ONE C-ABI call
+        (gw_rollout_step: Philox actions into self.actions, then the step with
+        the chosen auto-reset convention).  The pointer arguments are built
+        once per engine, so the host cost per step is one ctypes call.
+        Returns (obs, reward, done, all_done)."""
+        args = getattr(self, '_roll_args', None)
+        if args is None or args[0] != torch.cuda.current_stream().cuda_stream:
+            s = torch.cuda.current_stream().cuda_stream
+            args = self._roll_args = (s, _ptr(self.actions), _ptr(self.obs), _ptr(self.reward),
+                                      _ptr(self.done), _ptr(self.all_done), _ptr(self.acting),
+                                      _ptr(self.err), C.c_void_p(s))
+        st = self.L.gw_rollout_step(self.h, int(key) & 0xFFFFFFFFFFFFFFFF, int(step) & 0xFFFFFFFF,
+                                    int(env_offset) & 0xFFFFFFFF, *args[1:7], int(horizon),
+                                    self.AUTORESET_MODES[autoreset], *args[7:9])
+        if st != 0:
+            _native.check(st, 'gw_rollout_step')
+        return self.obs, self.reward, self.done, self.all_done
 
     def check_errors(self, allow=0):
         """Raise the reference's exception for the first env whose err flags

@@ -2,9 +2,14 @@
 
 Workload (BASELINE.json configs[2], the metric's config): TeamBattle 32x32,
 64 BattleAgents in 2 teams, 4096 envs per GPU (weak scaling: N GPUs run
-N x 4096 envs, sharded by global env id, no data-path collective), horizon
-200 with on-device auto-reset.  One timed "step" = random-policy actions
-(Philox kernel) + one fused AllStepManager.step launch for every env.
+N x 4096 envs, sharded by global env id, no data-path collective;
+--global-envs G: strong scaling, G envs in total), horizon 200 with
+on-device auto-reset.  One timed "step" = random-policy actions (Philox
+kernel) + one fused AllStepManager.step launch for every env.  Before the
+warmup, --preroll steps (default 1000, five horizons) run untimed so that
+the timed window is steady state: episodes at mixed phases, envs resetting
+inside the window.  --workload maze | rtt | pacman times BASELINE configs
+2, 4 and 5 instead (their own lines).
 
 Auto-reset (--autoreset): 'next_step' (default; gymnasium NEXT_STEP, the
 batched form of RLlib calling reset() after __all__: an env whose episode
@@ -35,40 +40,24 @@ sys.path.insert(0, ROOT)
 METRIC = json.load(open(os.path.join(ROOT, 'BASELINE.json')))['metric']
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+from abmarl_amd.examples.workloads import team_battle_sim, maze_sim, rtt_sim, pacman_sim  # noqa: E402
 
-def team_battle_sim(rows=32, cols=32, n_agents=64, n_teams=2):
-    from abmarl_amd.examples import BattleAgent, TeamBattleSim
-    agents = {f'agent{i}': BattleAgent(id=f'agent{i}', encoding=i % n_teams + 1)
-              for i in range(n_agents)}
-    return TeamBattleSim.build_sim(
-        rows, cols, agents=agents,
-        overlapping={t: {t} for t in range(1, n_teams + 1)},
-        attack_mapping={t: {u for u in range(1, n_teams + 1) if u != t}
-                        for t in range(1, n_teams + 1)},
-        states={'PositionState', 'HealthState'},
-        observers={'PositionCenteredEncodingObserver'},
-        dones={'OneTeamRemainingDone'})
+# the reference's own AllStepManager TeamBattle loop, measured in
+# the build container during the survey (pure Python, one process per core)
+REFERENCE_RATE_PER_CORE = 14.3e3
 
 
-def maze_sim():
-    """BASELINE config 2: MazeNavigation 16x16 (generated maze, blocking walls)."""
-    sys.path.insert(0, os.path.join(ROOT, 'tests'))
-    from tests.cases import load_golden, build_maze
-    return build_maze(load_golden('maze_16')['case'])
-
-
-def pacman_sim():
-    """BASELINE config 5: pacman.txt with four baddies (TurnBasedManager)."""
-    from abmarl_amd.examples.pacman import build_pacman
-    return build_pacman()
-
-
-def rtt_sim():
-    """BASELINE config 4: ReachTheTarget 64x64, 128 barriers + 127 runners +
-    the target (256 entities, the workgroup-per-env kernel)."""
-    sys.path.insert(0, os.path.join(ROOT, 'tests'))
-    from tests.cases import build_rtt, RTT_CONFIG4
-    return build_rtt(dict(RTT_CONFIG4))
+def host_cpu():
+    """CPU model and logical core count of this host (cpu_baseline)."""
+    model = 'unknown'
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
 
 
 def pacman_turn_bytes(E, A, HW, pwords):
@@ -130,14 +119,21 @@ def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200, mode='next_step'):
             o.reset(obs, all_done=ad, horizon=horizon)
         steps += 1
     dt = time.perf_counter() - t0
+    model, ncpu = host_cpu()
     return dict(value=float(acting.sum()) / dt, unit='agent-steps/s', cores=threads, kind='port',
                 sample=f'{envs} envs x {steps} steps, {mode} auto-reset (incl. action generation '
-                       f'in numpy), {dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads')
+                       f'in numpy), {dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads',
+                host_cpu=model, host_logical_cpus=ncpu,
+                note=('a C port of the reference step (oracle/), not the reference itself: the '
+                      'reference AllStepManager is pure Python and runs about '
+                      f'{REFERENCE_RATE_PER_CORE:.0f} agent-steps/s per core (SURVEY §6, measured in '
+                      'the build container); it cannot travel to the GPU box'))
 
 
-def quick_config(name, steps=200, warmup=20):
+def quick_config(name, steps=200, warmup=400):
     """A short single-GPU measurement of another BASELINE config (not the
-    metric's): agent-steps/s and the step kernel's average launch time."""
+    metric's): agent-steps/s and the step kernel's average launch time, after
+    an untimed pre-roll of `warmup` steps (two horizons: steady state)."""
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     if name == 'maze':
         cc, E, horizon = maze_sim().compiled(), 1024, 200
@@ -148,12 +144,13 @@ def quick_config(name, steps=200, warmup=20):
     eng = GridWorldEngine(cc, E, seeds=env_seeds(E))
     if name == 'maze' or name.startswith('rtt'):
         eng.reset()
-        eng.all_done.zero_()
         step = lambda: eng.step_autoreset_next(horizon=horizon)
     else:
         eng.turn_reset()
-        eng.all_done.zero_()
         step = lambda: eng.turn_step(horizon=horizon)
+    eng.all_done.zero_()
+    # episode phases spread over the horizon (as in the headline line)
+    eng.set_state(steps=torch.as_tensor((np.arange(E) * horizon // E).astype(np.int32), device=eng.device))
     key = 0x5eed0001
     for t in range(warmup):
         eng.random_actions(key, t)
@@ -174,7 +171,7 @@ def quick_config(name, steps=200, warmup=20):
     acting = int(eng.acting.sum().item()) - a0
     if name == 'maze':
         nbytes = step_bytes(E, eng.A, cc.obs_side)
-        desc = 'MazeNavigation 16x16 (maze_16 fixture map), 1024 envs, AllStep, next_step auto-reset'
+        desc = 'MazeNavigation 16x16 (workloads.MAZE_16), 1024 envs, AllStep, next_step auto-reset'
     elif name.startswith('rtt'):
         nbytes = rtt_step_bytes(E, eng.A, cc.obs_side, eng.act_dim)
         desc = (f'ReachTheTarget 64x64, 128 barriers + 127 runners + target (256 entities, '
@@ -191,22 +188,46 @@ def quick_config(name, steps=200, warmup=20):
             'achieved_GBs': round(nbytes / (kms * 1e-3) / 1e9, 2)}
 
 
+WORKLOADS = {
+    # name: (builder, default envs per GPU, step-kernel name, description)
+    'team_battle': (team_battle_sim, 4096, 'step_kernel<7>',
+                    'TeamBattle 32x32, 64 agents / 2 teams'),
+    'maze': (maze_sim, 1024, 'step_kernel<5>',
+             'MazeNavigation 16x16 (BASELINE config 2), 1 navigator, blocking walls'),
+    'rtt': (rtt_sim, 1024, 'wg_step_kernel<7>',
+            'ReachTheTarget 64x64 (BASELINE config 4), 256 entities'),
+    'pacman': (pacman_sim, 16384, 'pac_kernel',
+               'Pacman pacman.txt (BASELINE config 5), 4 baddies + pacman, TurnBasedManager'),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=500)
     ap.add_argument('--warmup', type=int, default=50)
-    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    ap.add_argument('--preroll', type=int, default=1000,
+                    help='untimed steps before the warmup, so the timed window is steady state '
+                         '(episodes at mixed phases, auto-resets inside the window)')
+    ap.add_argument('--envs', type=int, default=0, help='envs per GPU (weak scaling; default: the workload\'s)')
+    ap.add_argument('--global-envs', type=int, default=0,
+                    help='strong scaling: this many envs in total, sharded over the ranks')
     ap.add_argument('--horizon', type=int, default=200)
+    ap.add_argument('--no-stagger', action='store_true',
+                    help='start every episode at step 0 (default: the first episode of global env '
+                         'e starts at step e * horizon // envs, so horizon resets are spread over '
+                         'the steps instead of all envs resetting together every horizon)')
+    ap.add_argument('--event-every', type=int, default=4,
+                    help='HIP events around the step kernel of every n-th timed step (the others '
+                         'go through the one-call gw_rollout_step path)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--autoreset', choices=['next_step', 'same_step'], default='next_step')
     ap.add_argument('--no-other', action='store_true',
                     help='skip the other auto-reset mode and the other configs')
-    ap.add_argument('--workload', choices=['team_battle', 'rtt'], default='team_battle',
-                    help="'rtt': BASELINE config 4 (ReachTheTarget 64x64, 256 entities; "
-                         "--envs 1024 = one GPU's share of 8192) as the timed workload, "
-                         "for profiling its kernel (not the headline metric)")
+    ap.add_argument('--workload', choices=sorted(WORKLOADS), default='team_battle',
+                    help="the timed workload; the metric's is team_battle (BASELINE configs[2]); the "
+                         "others are BASELINE configs 2, 4, 5 (their own lines, not the headline metric)")
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -221,49 +242,76 @@ def main():
     from abmarl_amd import _abi
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     from abmarl_amd.parallel import shard_envs, gather_episode_stats
-    sim = team_battle_sim() if args.workload == 'team_battle' else rtt_sim()
+    builder, default_envs, kname, wdesc = WORKLOADS[args.workload]
+    sim = builder()
     cc = sim.compiled()
-    if args.workload == 'rtt' and args.envs == 4096:
-        args.envs = 1024
-    first, E_local = shard_envs(args.envs * world, rank, world)
+    turn = args.workload == 'pacman'
+    strong = args.global_envs > 0
+    total_envs = args.global_envs if strong else (args.envs or default_envs) * world
+    first, E_local = shard_envs(total_envs, rank, world)
     key = 0x5eed0000  # policy key shared by all ranks; global env ids make streams distinct
+    allow = _abi.GW_ERR_DOUBLE_REMOVE if args.workload == 'rtt' else 0
+    untimed = args.preroll + args.warmup
 
     def run(mode):
-        """Fresh engine (same seeds), warmup, then K timed steps."""
+        """Fresh engine (same seeds), pre-roll + warmup, then K timed steps."""
         eng = GridWorldEngine(cc, E_local, seeds=env_seeds(E_local, run=0, first_env=first))
-        eng.reset()
+        if turn:
+            eng.turn_reset()
+        else:
+            eng.reset()
         eng.all_done.zero_()
+        if not args.no_stagger:
+            # episode phases spread over the horizon by global env id: the
+            # horizon resets (most TeamBattle episodes end there) land on
+            # every step instead of all envs together, so any window of the
+            # rollout, however short, is steady state
+            gid = np.arange(first, first + E_local, dtype=np.int64)
+            eng.set_state(steps=torch.as_tensor((gid * args.horizon // total_envs).astype(np.int32),
+                                                device=eng.device))
         torch.cuda.synchronize()
         eng.check_errors()
-        step = eng.step_autoreset_next if mode == 'next_step' else eng.step_autoreset
-
-        def one_step(t, ev=None):
-            eng.random_actions(key, t, env_offset=first)
-            if ev is not None:
-                ev[0].record()
-            step(horizon=args.horizon)
-            if ev is not None:
-                ev[1].record()
-
-        for t in range(args.warmup):
-            one_step(t)
+        step = (lambda: eng.turn_step(horizon=args.horizon)) if turn else \
+            (eng.step_autoreset_next if mode == 'next_step' else eng.step_autoreset)
+        for t in range(untimed):
+            if turn:
+                eng.random_actions(key, t, env_offset=first)
+                step()
+            else:
+                eng.rollout_step(key, t, env_offset=first, horizon=args.horizon, autoreset=mode)
         torch.cuda.synchronize()
         # ReachTheTarget: a runner placed on the target's cell and killed there
         # raises the reference's KeyError; the auto-reset modes reset that env
-        eng.check_errors(allow=_abi.GW_ERR_DOUBLE_REMOVE if args.workload == 'rtt' else 0)
+        eng.check_errors(allow=allow)
+        every = max(1, args.event_every)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
+               for _ in range(0, args.steps, every)]
         acting0 = int(eng.acting.sum().item())
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for t in range(args.steps):
-            one_step(args.warmup + t, evs[t])
+            if turn or t % every == 0:
+                # HIP events on the launch stream around the step kernel
+                eng.random_actions(key, untimed + t, env_offset=first)
+                ev = evs[t // every] if t % every == 0 else None
+                if ev:
+                    ev[0].record()
+                if turn:
+                    step()
+                else:
+                    step(horizon=args.horizon)
+                if ev:
+                    ev[1].record()
+            else:
+                eng.rollout_step(key, untimed + t, env_offset=first, horizon=args.horizon,
+                                 autoreset=mode)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         dt = time.perf_counter() - t0
+        eng.check_errors(allow=allow)
         acting = int(eng.acting.sum().item()) - acting0
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
@@ -276,32 +324,48 @@ def main():
         return eng, dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
                          step_ms=step_ms, step_ms_max=kms[0].item())
 
-    other = 'same_step' if args.autoreset == 'next_step' else 'next_step'
-    eng, r = run(args.autoreset)
-    A, S = eng.A, cc.obs_side
+    mode = 'next_step' if turn else args.autoreset
+    other = 'same_step' if mode == 'next_step' else 'next_step'
+    eng, r = run(mode)
+    A, n_passive = eng.A, eng.n_passive
     stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
     del eng
-    r2 = None if args.no_other else run(other)[1]
-    acting_all, dt_all, envs_all, step_ms = r['acting'], r['dt'], r['envs'], r['step_ms']
+    r2 = None if (args.no_other or turn) else run(other)[1]
+    acting_all, dt_all, envs_all = r['acting'], r['dt'], r['envs']
     step_ms_all = r['step_ms_max']
 
     if rank == 0:
         value = acting_all / dt_all
-        nbytes = step_bytes(E_local, A, S)
-        kname = 'step_kernel<7>'
-        workload = ('TeamBattle 32x32, 64 agents / 2 teams, 4096 envs per GPU, '
-                    f'horizon 200, {args.autoreset} auto-reset')
-        if args.workload == 'rtt':
+        S = cc.obs_side
+        if args.workload == 'team_battle' or args.workload == 'maze':
+            nbytes = step_bytes(E_local, A, S)
+        elif args.workload == 'rtt':
             nbytes = rtt_step_bytes(E_local, A, S, cc.act_dim)
-            kname = 'wg_step_kernel<7>'
-            workload = (f'ReachTheTarget 64x64 (BASELINE config 4), 256 entities, {E_local} envs per GPU, '
-                        f'horizon 200, {args.autoreset} auto-reset (profiling run, not the headline metric)')
-        achieved = nbytes / (step_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, 'profiles', 'pmc_step_kernel.json' if args.workload == 'team_battle'
-                           else 'pmc_wg_step_kernel.json')
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+        else:
+            nbytes = pacman_turn_bytes(E_local, A, cc.rows * cc.cols, (n_passive + 31) // 32)
+        scaling = 'strong' if strong else 'weak'
+        workload = (f'{wdesc}, {E_local} envs per GPU ({int(envs_all)} in total, {scaling} scaling), '
+                    f'horizon {args.horizon}, {mode} auto-reset, {args.preroll}-step pre-roll')
+        if args.workload != 'team_battle':
+            workload += ' (not the headline metric\'s config)'
+        achieved = nbytes / (step_ms_all * 1e-3) / 1e9
+        traffic, rocprof_ms = None, None
+        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}.json')
+        if args.workload == 'team_battle' and os.path.exists(pmc):
+            prof = json.load(open(pmc))
+            traffic = prof.get('hbm_bytes_per_launch')
+            rocprof_ms = prof.get('rocprof_avg_ms')
+        roof = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
+                'traffic': traffic, 'kernel': kname, 'kernel_ms': round(step_ms_all, 4),
+                'kernel_timing': f'HIP events around the step kernel of every {max(1, args.event_every)}'
+                                 f'-th timed step (launch stream), mean; max over ranks',
+                'bytes_per_launch': nbytes}
+        if rocprof_ms:
+            # the same ratio with the committed rocprofv3 kernel-trace average
+            # (no event / dispatch time in it)
+            roof['rocprof_kernel_ms'] = rocprof_ms
+            roof['frac_rocprof'] = round(nbytes / (rocprof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
         out = {
             'metric': METRIC,
             'value': round(value, 1),
@@ -309,31 +373,30 @@ def main():
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
+            'preroll_steps': args.preroll,
+            'stagger': None if args.no_stagger else
+            'first episode of global env e starts at step e*horizon//envs',
             'ms_per_step': round(dt_all / args.steps * 1e3, 4),
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': scaling,
             'vs_baseline': None,
             'dtype': 'int32 (positions/obs), f64 (health/reward)',
-            'data': 'synthetic: Philox random-policy actions, random-init TeamBattle episodes',
+            'data': 'synthetic: Philox random-policy actions, random-init episodes',
             'config': {'workload': workload,
                        'envs_per_gpu': E_local, 'global_envs': int(envs_all),
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
             'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                         'traffic': traffic, 'kernel': kname,
-                         'kernel_ms': round(step_ms_all, 4),
-                         'bytes_per_launch': nbytes},
+            'roofline': roof,
             'episode_stats': stats,
-            'autoreset': args.autoreset,
+            'autoreset': mode,
             'other_autoreset': None if r2 is None else {
                 'mode': other, 'value': round(r2['acting'] / r2['dt'], 1),
                 'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
                 'kernel_ms': round(r2['step_ms_max'], 4)},
         }
         if world == 1 and not args.no_other and args.workload == 'team_battle':
-            # BASELINE configs 2 and 5 (single GPU, short runs; not the metric)
+            # BASELINE configs 2, 4 and 5 (single GPU, short runs; not the metric)
             out['other_configs'] = {'maze_16': quick_config('maze'),
                                     'reach_the_target_64': quick_config('rtt'),
                                     'reach_the_target_64_all_8192': quick_config('rtt_8192'),

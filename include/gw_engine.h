@@ -180,6 +180,17 @@ typedef struct gw_config {
     int32_t  pacman_agent;         /* index of 'pacman' (else -1)               */
     int32_t  tunnel[4];            /* r0, c0, r1, c1: the teleporting cells (pacman.py:88-93) */
     double   pac_rewards[5];       /* reward_scheme: bad_move, entropy, eat_food, kill, die */
+    /* kernel selection: 0 = automatic (one wave per env; ReachTheTarget with
+       more than GW_MAX_AGENTS lanes on a workgroup per env), 1 = force the
+       workgroup-per-env kernel (ReachTheTarget; parity tests run the small
+       reference fixtures through it)                                         */
+    int32_t  force_workgroup;
+    /* 1: the caller passes the SAME obs buffer to every call of this handle
+       (as the Python engine does with its own), so the one-wave kernels do
+       not rewrite the rows that already hold -2 and stay -2 (entities done
+       before this step, non-observers): steady-state obs stores shrink with
+       the done fraction.  0: every row is written every call.              */
+    int32_t  persistent_obs;
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack
@@ -215,7 +226,11 @@ gw_status gw_seed(gw_handle h, const uint32_t* seeds, void* stream);
      mask      device uint8[E] or NULL
      all_done  device uint8[E] or NULL  (the previous step's __all__)
      obs       device int32[E][A][S][S], S = 2*obs_range+1
-     err_flags device uint32[E] (OR-ed GW_ERR_*)                              */
+     err_flags device uint32[E]: a reset env's flags are replaced by the
+               reset's own (GW_ERR_NO_CELL / GW_ERR_INIT_POSITION or 0), so
+               an error raised before the reset does not outlive it; flags
+               of envs not reset are untouched.  (gw_turn_reset and
+               gw_sim_reset do the same.)                                   */
 gw_status gw_reset(gw_handle h, const uint8_t* mask, const uint8_t* all_done,
                    int32_t horizon, int32_t* obs, uint32_t* err_flags, void* stream);
 
@@ -275,6 +290,16 @@ gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
    the reference; it is the benchmark's synthetic policy.                     */
 gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
                             int32_t* actions, void* stream);
+
+/* One step of a synthetic random-policy rollout in one call: gw_random_actions
+   into `actions`, then on the same stream gw_step (autoreset 0),
+   gw_step_autoreset (1) or gw_step_autoreset_next (2) on those actions.  The
+   outputs are those of the step call.  (AllStepManager protocol; the Pacman
+   program's turn-based protocol is gw_turn_step.)                           */
+gw_status gw_rollout_step(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
+                          int32_t* actions, int32_t* obs, double* reward, uint8_t* done,
+                          uint8_t* all_done, uint64_t* acting, int32_t horizon, int32_t autoreset,
+                          uint32_t* err_flags, void* stream);
 
 /* ---------------------------------------------------------------------
  * Pacman program (GW_SIM_PACMAN): the turn-based and simulation-only

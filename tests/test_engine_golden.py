@@ -16,12 +16,13 @@ class EngineRunner:
     reference reports them: obs -2 (not an observer), reward 0, done 1 (not
     an Agent), at their initial position, active, health 0."""
 
-    def __init__(self, g):
+    def __init__(self, g, force_workgroup=False):
         import torch
         from abmarl_amd.engine import GridWorldEngine
         self.torch = torch
         c = g['case']
         self.cc = golden_config(g)
+        self.cc.cfg.force_workgroup = int(force_workgroup)
         self.eng = GridWorldEngine(self.cc, c['n_envs'], seeds=c['seeds'])
         self.NE = self.cc.n_agents
         self.lanes = self.eng.lane_entities
@@ -106,10 +107,11 @@ RTT_GOLDEN = [n for n in GOLDEN_CASES if n.startswith('rtt')]
 
 
 @pytest.mark.parametrize('name', RTT_GOLDEN)
-def test_engine_workgroup_kernel_matches_reference(name, monkeypatch):
+def test_engine_workgroup_kernel_matches_reference(name):
     """The ReachTheTarget workgroup-per-env kernel (gw_rtt.inc) on every RTT
-    fixture, the small ones included (GW_RTT_KERNEL=wg; config 4's size takes
-    it anyway)."""
-    monkeypatch.setenv('GW_RTT_KERNEL', 'wg')
+    fixture, the small ones included (gw_config.force_workgroup; config 4's
+    size takes it anyway)."""
     g = load_golden(name)
-    replay(EngineRunner(g), g)
+    r = EngineRunner(g, force_workgroup=True)
+    assert r.eng.wg
+    replay(r, g)

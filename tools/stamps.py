@@ -45,7 +45,11 @@ def report(st, order, names, title):
 TB_STEP = {0: 'start', 10: 'prologue', 1: 'tables', 7: 'attack precheck', 2: 'attack loop',
            11: 'move isolation', 3: 'serial moves+table', 4: '-',
            8: 'obs windows', 9: 'crowded draws', 5: 'obs store', 6: 'dones+store'}
-TB_NEXT = {0: 'start', 10: 'prologue', 12: '-', 13: 'placement+health', 14: 'tables+obs', 6: 'store'}
+TB_NEXT = {0: 'start', 10: 'prologue', 12: '-', 11: 'placement', 15: 'health', 13: '-',
+           26: 'tables+obs windows', 27: 'crowded draws', 14: 'obs store', 6: 'state store'}
+
+
+NSTEPS = int(os.environ.get('NSTEPS', '430'))
 
 
 def main():
@@ -64,22 +68,29 @@ def main():
         sw = st[:, 21]
         print(f'{"sweeps":>24}: median {np.median(sw):.0f} max {sw.max()}')
     eng.all_done.zero_()
-    for t in range(30):
+    # episode phases spread over the horizon, as in bench.py (steady state:
+    # about E/200 envs reset in every launch)
+    H = 200
+    eng.set_state(steps=torch.as_tensor((np.arange(E) * H // E).astype(np.int32), device=eng.device))
+    for t in range(NSTEPS):
         eng.random_actions(1, t)
         eng.stamps.zero_()
-        eng.step_autoreset_next(horizon=200)
+        eng.step_autoreset_next(horizon=H)
     torch.cuda.synchronize()
     st = eng.stamps.cpu().numpy()
     if wl == 'rtt':
-        report(st, list(range(10)), STEP, f'{wl}: step launch 30 (next_step auto-reset)')
+        report(st, list(range(10)), STEP, f'{wl}: step launch {NSTEPS} (next_step auto-reset)')
         tot = st[:, 9] - st[:, 0]
     else:
         stepped = st[:, 2] != 0
         report(st[stepped], [0, 10, 1, 7, 2, 11, 3, 4, 8, 9, 5, 6], TB_STEP,
-               f'{wl}: step launch 30, stepping envs ({stepped.sum()})')
+               f'{wl}: step launch {NSTEPS}, stepping envs ({stepped.sum()})')
         if (~stepped).any():
-            report(st[~stepped], [0, 10, 12, 13, 14, 6], TB_NEXT, f'{wl}: resetting envs ({(~stepped).sum()})')
+            report(st[~stepped], [0, 10, 12, 11, 15, 13, 26, 27, 14, 6], TB_NEXT,
+                   f'{wl}: resetting envs ({(~stepped).sum()})')
         tot = st[:, 6] - st[:, 0]
+        print(f'launch span (last end - first start, if the counter is global): '
+              f'{st[:, 6].max() - st[:, 0].min()} ticks; starts spread over {st[:, 0].max() - st[:, 0].min()}')
     if wl != 'rtt':
         ns, na = st[:, 28], st[:, 29]
         at = st[:, 2] - st[:, 1]
