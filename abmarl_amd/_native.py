@@ -40,6 +40,7 @@ SIGNATURES = {
     'gw_random_actions': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp]),
     'gw_rollout_step': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
                                _vp, _vp]),
+    'gw_rollout': (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     'gw_destroy': (_i32, [_vp]),
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),
@@ -64,13 +65,13 @@ SIGNATURES = {
 PART_SIDES = (1, 3, 5, 7, 9, 11, 13, 15)   # observation window sides S = 2*range+1
 
 
-def build(force=False, verbose=False, stamps=False, checks=False):
+def build(force=False, verbose=False, stamps=False, checks=False, out=None, extra_flags=()):
     """Compile the engine for gfx950 with hipcc (works without a GPU).
 
     gw_engine.hip is compiled as one host part plus one part per window side
     S (-DGW_PART_S, the templated step/reset kernels), in parallel, then
     linked into one shared library."""
-    out = LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB)
+    out = out or (LIB_STAMPS if stamps else (LIB_CHECKS if checks else LIB))
     csrc = os.path.dirname(SRC)
     deps = [SRC, INCLUDE] + [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith('.inc')]
     if not force and os.path.exists(out) and \
@@ -78,9 +79,11 @@ def build(force=False, verbose=False, stamps=False, checks=False):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tag = 'stamps' if stamps else ('checks' if checks else 'prod')
+    if extra_flags:   # tools' A/B builds (tools/ab_lib.py)
+        tag = os.path.splitext(os.path.basename(out))[0]
     flags = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-ffp-contract=off', '-fPIC',
              '-Wno-unused-result'] + (['-DGW_STAMPS'] if stamps else []) + \
-        (['-DGW_CHECKS'] if checks else [])
+        (['-DGW_CHECKS'] if checks else []) + list(extra_flags)
     objdir = os.path.join(os.path.dirname(out), f'obj_{tag}')
     os.makedirs(objdir, exist_ok=True)
     jobs = [(os.path.join(objdir, 'host.o'), [])] + \

@@ -130,6 +130,12 @@ struct Params {
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
     int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
     int32_t persistent_obs;                // gw_config.persistent_obs: skip rows already -2
+    // gw_rollout: steps per launch (1 for the single-step calls), the
+    // previous call's __all__ (NEXT_STEP input; the single-step calls pass
+    // all_done itself), rows of lanes without an observation left unwritten
+    int32_t nsteps;
+    const uint8_t* ad_in;
+    int32_t skip_done_obs;
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -236,12 +242,13 @@ __device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
 }
 
 // ------------------------------------------------------------ diagnostics
+#define GW_STAMP_STRIDE 64   // stamps[E][64] (tools/stamps.py)
 #ifdef GW_STAMPS
 #define STAMP(i)                                                                  \
     do {                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                        \
         uint64_t _t = __builtin_amdgcn_s_memtime();                               \
-        if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * 32 + (i)] = _t;      \
+        if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * GW_STAMP_STRIDE + (i)] = _t;      \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
 #else
@@ -611,7 +618,7 @@ __host__ __device__ constexpr int stage_pitch(int S) { return (S + 3) & ~3; }
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S>
 __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
-                                            int stamp_base = 8)
+                                            int32_t* obs, int stamp_base = 8)
 {
     (void)stamp_base;
     constexpr int SS = S * S;
@@ -625,8 +632,11 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
     // persistent obs buffer (gw_config.persistent_obs): rows that already
     // hold -2 and stay -2 (done entities, non-observers) are not rewritten
-    const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me) : 0ull;
-    if (l < A) L.obs_m2 = !obs_me;
+    // (gw_rollout with skip_done_obs: rows of lanes without an observation
+    // this step are not written at all)
+    const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me)
+                        : (p.skip_done_obs ? __ballot(l < A && !obs_me) : 0ull);
+    if (l < A) L.obs_m2 = p.persistent_obs && !obs_me;
 
     // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
     // static blockers precomputed per cell, blocking lanes from the shadow LUT
@@ -859,7 +869,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     // when rows are padded by one byte (S = 7, 11, 15) four consecutive
     // outputs lie within two stage dwords: one byte-permute.
     const int total = A * SS;
-    int32_t* out = p.obs + (size_t)e * total;
+    int32_t* out = obs + (size_t)e * total;
     if (S >= 4 && SP - S <= 1 && (total & 3) == 0) {
         constexpr int NIT = (GW_MAX_AGENTS * SS + 4 * WAVE - 1) / (4 * WAVE);
         constexpr int B = NIT < 7 ? NIT : 7;                    // LDS reads in flight
@@ -1256,24 +1266,42 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const bool randh = hl && !(L.init_health >= 0.0);
         const uint64_t rm = __ballot(randh);
         const int nrand = __popcll(rm);
-        if (rng.pos + 2 * nrand <= GW_MT_N) {
+#ifdef GW_STAMPS
+        if (l == 0 && p.stamps) {
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 40] = (uint64_t)rng.pos;
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 41] = (uint64_t)nrand;
+        }
+#endif
+        if (rng.pos + 2 * nrand <= 2 * GW_MT_N) {
+            // the lane of random-health rank k takes stream words pos + 2k and
+            // pos + 2k + 1; words past the key's end come from the twisted
+            // key (numpy twists when the position reaches 624, mt19937.c)
+            const int k = __popcll(rm & ((1ull << l) - 1));
+            const int i0 = rng.pos + 2 * k;
+            uint32_t w[2] = {0u, 0u};
+#pragma unroll
+            for (int q = 0; q < 2; q++)
+                if (randh && i0 + q < GW_MT_N) w[q] = temper(rng.key[CIDX(i0 + q, GW_MT_N, 5)]);
+            const int np = rng.pos + 2 * nrand;
+            if (np > GW_MT_N) {
+                mt_twist(rng.key);
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    if (randh && i0 + q >= GW_MT_N) w[q] = temper(rng.key[CIDX(i0 + q - GW_MT_N, GW_MT_N, 5)]);
+                rng.pos = np - GW_MT_N;
+                rng.dirty = true;
+                rng.base = -1;
+            } else {
+                rng.pos = np;
+            }
             if (hl) {
                 double h = L.init_health;
-                if (randh) {
-                    const int k = __popcll(rm & ((1ull << l) - 1));
-                    uint32_t w[2];
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        w[q] = temper(rng.key[CIDX(rng.pos + 2 * k + q, GW_MT_N, 5)]);
-                    }
-                    h = ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6)) / 9007199254740992.0;
-                }
+                if (randh) h = ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6)) / 9007199254740992.0;
                 if (0.0 > h) h = 0.0;
                 if (1.0 < h) h = 1.0;
                 L.health = h;
                 L.active = h > 0.0;
             }
-            rng.pos += 2 * nrand;
             return;
         }
         for (int a = 0; a < A; a++) {
@@ -1359,7 +1387,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         if (L.in_grid) { const int gc = to_cell(cell_l); L.r = gc / p.W; L.c = gc % p.W; }
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps)
-            for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * 32 + 16 + k] = acc_t[k];
+            for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 16 + k] = acc_t[k];
 #endif
         return true;
     };
@@ -1602,8 +1630,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         ACC_T(4, t0);
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps) {
-            for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * 32 + 20 + k] = acc_t[k];
-            p.stamps[(size_t)blockIdx.x * 32 + 25] = nsw;
+            for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 25] = nsw;
         }
 #endif
         return 0;
@@ -1635,7 +1663,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
 
 template <int S>
 __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr,
-                                          bool fused)
+                                          bool fused, int32_t* obs)
 {
     constexpr int SS = S * S;
     uint32_t err = 0;
@@ -1652,20 +1680,44 @@ __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng&
             wave_sync();
         }
         build_tables(p, sm, L, !fused);
-        observe_all<S>(p, e, sm, rng, L, 26);
+        observe_all<S>(p, e, sm, rng, L, obs, 26);
     } else {
-        int32_t* out = p.obs + (size_t)e * p.A * SS;
+        int32_t* out = obs + (size_t)e * p.A * SS;
         for (int i = lane_id(); i < p.A * SS; i += WAVE) out[i] = -2;
+        if (lane_id() < p.A) L.obs_m2 = p.persistent_obs != 0;
     }
-    if (lane_id() == 0) {
-        p.steps[e] = 0;
-        if (p.err) p.err[e] |= err;
-    }
+    if (lane_id() == 0 && p.err) p.err[e] |= err;
+}
+
+// the per-config template (static entities, off-grid border) in the LDS
+// table without any lane, counts zeroed
+__device__ __forceinline__ void table_template(const Params& p, Smem& sm)
+{
+    const int l = lane_id();
+    wave_sync();
+    const int t16 = (p.tbl_rows * p.pitch + 15) / 16;
+    for (int i = l; i < t16; i += WAVE) ((uint4*)sm.tbl)[i] = p.tbl_tmpl[i];
+    const int nw = (p.H * p.W + 3) / 4;
+    for (int i = l; i < nw; i += WAVE) sm.cnt[i] = 0u;
+    wave_sync();
 }
 
 // ------------------------------------------------------------ kernels
+// AllStepManager.step for p.nsteps consecutive steps of one env (one wave):
+// the single-step calls run one; gw_rollout runs a whole fragment of a
+// rollout in one launch, so each env goes on to its next step as soon as it
+// has finished one (no launch-wide barrier between steps: the launch lasts
+// the slowest env's SUM of steps, not the sum of every step's slowest env).
+// Lane state, the RNG (key in LDS once loaded) and the LDS cell table stay
+// on the chip between steps; step t reads actions[t] and writes obs[t],
+// reward[t], done[t], all_done[t] (strides E*A*act_dim, E*A*SS, E*A, E).
+// waves per SIMD the step kernel is compiled for: 4 keeps it within 128
+// VGPRs, so 16 one-wave envs (the LDS limit at TeamBattle's size) share a CU
+#ifndef GW_STEP_WAVES_PER_EU
+#define GW_STEP_WAVES_PER_EU 4
+#endif
 template <int S>
-__global__ __launch_bounds__(WAVE) void step_kernel(Params p)
+__global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params p)
 {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int e = blockIdx.x;
@@ -1673,313 +1725,340 @@ __global__ __launch_bounds__(WAVE) void step_kernel(Params p)
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
+    constexpr int SS = S * S;
     STAMP(0);
     Smem sm = carve(smem_raw, p);
     // every global load of the prologue is issued before any is used (one
     // memory round trip): the epilogue counters, the previous __all__ (read
     // unconditionally: a branch on it would wait for it), lanes, actions
     const int32_t steps_raw = p.steps[e];
-    const uint32_t ad_raw = p.all_done[e];
+    const uint32_t ad_raw = p.ad_in ? p.ad_in[e] : 0u;
     Lane L;
     load_lane(p, e, L, valid);
     // actions (lane = agent); attack == -1 marks "not in action_dict"
+    const size_t EA = (size_t)p.E * A;
+    const size_t act_row = ((size_t)e * A + (valid ? l : 0)) * p.act_dim;
     int mr, mc, ak;
     {
-        const int32_t* ap = p.actions + ((size_t)e * A + (valid ? l : 0)) * p.act_dim;
+        const int32_t* ap = p.actions + act_row;
         const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
         mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
     }
-    const uint64_t acting0 = p.acting ? p.acting[e] : 0ull;
+    const uint64_t acting_raw = p.acting ? p.acting[e] : 0ull;
     Rng rng;
     uint32_t ctr;
     load_env(p, e, sm, rng, ctr, true);
-    const int32_t steps0 = uni(steps_raw);
-    const bool next_reset = p.autoreset == 2 && (uni(ad_raw) != 0u || (p.horizon > 0 && steps0 >= p.horizon));
-    if (next_reset) {
-        // NEXT_STEP auto-reset: the episode ended in the previous call, so
-        // this call is AllStepManager.reset for the env (actions ignored):
-        // obs = first observation, reward 0, done = not an Agent, no __all__.
-        // The LDS table holds the template (load_env), as after a step.
-        // The reset is the launch's critical path: issue it ahead of the
-        // SIMD's stepping waves.
-        __builtin_amdgcn_s_setprio(3);
-        STAMP(10);
-        STAMP(12);
-        reset_env<S>(p, e, sm, rng, L, ctr, true);
-        STAMP(14);
-        if (valid) {
-            const size_t k = (size_t)e * A + l;
-            p.reward[k] = 0.0;
-            p.done[k] = L.live ? (uint8_t)0 : (uint8_t)1;
+    int32_t steps = uni(steps_raw);
+    uint64_t acting_sum = 0;
+    bool prev_all = uni(ad_raw) != 0u;
+    // the LDS table holds the template (load_env); lanes are added before
+    // the first step that needs them (a reset adds its own)
+    bool lanes_in = false, need_tmpl = false;
+    for (int t = 0; t < p.nsteps; t++) {
+        const int32_t* act_t = p.actions + (size_t)t * EA * p.act_dim;
+        int32_t* obs_t = p.obs + (size_t)t * EA * SS;
+        double* rew_t = p.reward + (size_t)t * EA;
+        uint8_t* done_t = p.done + (size_t)t * EA;
+        uint8_t* ad_t = p.all_done + (size_t)t * p.E;
+        if (t > 0) {
+            const int32_t* ap = act_t + act_row;
+            const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
+            mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
         }
-        if (l == 0) p.all_done[e] = 0;
-        store_lane(p, e, L, valid);
-        store_rng(p, e, sm, rng, ctr);
-        STAMP(6);
-        return;
-    }
-    if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
-    const bool acting = valid && L.live && ak >= 0;
-    const uint64_t act_mask = __ballot(acting);
-    STAMP(10);
-    build_tables(p, sm, L, false);
-    STAMP(1);
+        if (need_tmpl) { table_template(p, sm); lanes_in = false; need_tmpl = false; }
+        // NEXT_STEP auto-reset: the episode ended in the previous step, so this
+        // step is AllStepManager.reset for the env (actions ignored): obs =
+        // first observation, reward 0, done = not an Agent, no __all__
+        const bool next_reset = p.autoreset == 2 && (prev_all || (p.horizon > 0 && steps >= p.horizon));
+        bool reset_now = next_reset;
+        if (!next_reset) {
+            if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
+            const bool acting = valid && L.live && ak >= 0;
+            const uint64_t act_mask = __ballot(acting);
+            STAMP(10);
+            if (!lanes_in) { build_tables(p, sm, L, false); lanes_in = true; }
+            STAMP(1);
+            L.reward = 0.0;
+            bool raised = false;                 // ReachTheTarget's double remove (KeyError)
 
-    if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
-        // ---- attack pass (team_battle_example.py:35-47)
-        const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
-        const bool maybe = att && L.active && attack_precheck(p, sm, L);
-        const uint64_t maybe_mask = __ballot(maybe);
-        // the launch lasts as long as its slowest env: an env with a long
-        // serial attack chain gets issue priority over the SIMD's other waves
-        {
-            const int nser = __popcll(maybe_mask);
-            if (nser >= 16) __builtin_amdgcn_s_setprio(2);
-            else if (nser >= 8) __builtin_amdgcn_s_setprio(1);
-#ifdef GW_STAMPS
-            const int natt = __popcll(__ballot(att));
-            if (l == 0 && p.stamps) {
-                p.stamps[(size_t)e * 32 + 28] = nser;
-                p.stamps[(size_t)e * 32 + 29] = natt;
-            }
-#endif
-        }
-        STAMP(7);
-        // Only attackers with a possible target run serially.  The others get
-        // (True, []) -> -0.1 if still active at their turn: applied lane-parallel
-        // just before the next serial attacker after them (so each lane's
-        // reward terms keep their reference order), or after the loop.
-        uint64_t pend = __ballot(att) & ~maybe_mask;
-        for (uint64_t it = maybe_mask; it; it &= it - 1) {
-            const int a = first_lane(it);
-            const uint64_t before = pend & ((1ull << a) - 1ull);
-            if (before) {
-                if (((before >> l) & 1ull) && L.active) L.reward -= 0.1;
-                pend &= ~before;
-            }
-            if (!rlb(L.active, a)) continue;                // killed earlier this pass
-            int nlist, list;
-            attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
-            if (nlist == 0) { if (l == a) L.reward -= 0.1; }
-            else {
-                for (int t = 0; t < nlist; t++) {
-                    const int b = rl(list, t);
-                    if (!rlb(L.active, b)) {
-                        if (l == b) L.reward -= 1.0;
-                        if (l == a) L.reward += 1.0;
+            if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
+                // ---- attack pass (team_battle_example.py:35-47)
+                const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
+                const bool maybe = att && L.active && attack_precheck(p, sm, L);
+                const uint64_t maybe_mask = __ballot(maybe);
+                // the launch lasts as long as its slowest env: an env with a long
+                // serial attack chain gets issue priority over the SIMD's other waves
+                {
+                    const int nser = __popcll(maybe_mask);
+                    if (nser >= 16) __builtin_amdgcn_s_setprio(2);
+                    else if (nser >= 8) __builtin_amdgcn_s_setprio(1);
+        #ifdef GW_STAMPS
+                    const int natt = __popcll(__ballot(att));
+                    if (l == 0 && p.stamps) {
+                        p.stamps[(size_t)e * GW_STAMP_STRIDE + 28] = nser;
+                        p.stamps[(size_t)e * GW_STAMP_STRIDE + 29] = natt;
+                    }
+        #endif
+                }
+                STAMP(7);
+                // Only attackers with a possible target run serially.  The others get
+                // (True, []) -> -0.1 if still active at their turn: applied lane-parallel
+                // just before the next serial attacker after them (so each lane's
+                // reward terms keep their reference order), or after the loop.
+                uint64_t pend = __ballot(att) & ~maybe_mask;
+                for (uint64_t it = maybe_mask; it; it &= it - 1) {
+                    const int a = first_lane(it);
+                    const uint64_t before = pend & ((1ull << a) - 1ull);
+                    if (before) {
+                        if (((before >> l) & 1ull) && L.active) L.reward -= 0.1;
+                        pend &= ~before;
+                    }
+                    if (!rlb(L.active, a)) continue;                // killed earlier this pass
+                    int nlist, list;
+                    attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                    if (nlist == 0) { if (l == a) L.reward -= 0.1; }
+                    else {
+                        for (int t = 0; t < nlist; t++) {
+                            const int b = rl(list, t);
+                            if (!rlb(L.active, b)) {
+                                if (l == b) L.reward -= 1.0;
+                                if (l == a) L.reward += 1.0;
+                            }
+                        }
                     }
                 }
-            }
-        }
-        if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
-        STAMP(2);
-        // ---- move pass (:50-55)
-        const bool mover = acting && L.active;
-        const bool can_move = mover && (L.kind & GW_K_MOVING);
-        const int nr = L.r + mr, nc = L.c + mc;
-        const bool inb = 0 <= nr && nr < p.H && 0 <= nc && nc < p.W;
-        const bool stay = nr == L.r && nc == L.c;
-        const bool real = can_move && inb && !stay;
-        // isolation: no other mover targets my source or target, none leaves my target
-        const int HW = p.H * p.W;
-        const int nw = (HW + 3) / 4;
-        for (int i = l; i < nw; i += WAVE) { sm.tcnt[i] = 0u; sm.scnt[i] = 0u; }
-        wave_sync();
-        const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
-        if (real) {
-            atomicAdd(&sm.tcnt[cnt_word(p, tgt)], 1u << (8 * (tgt & 3)));
-            atomicAdd(&sm.scnt[cnt_word(p, src)], 1u << (8 * (src & 3)));
-        }
-        wave_sync();
-        bool iso = false, iso_ok = false;
-        if (real && cnt_get(sm.tcnt, tgt) == 1 && cnt_get(sm.scnt, tgt) == 0 &&
-            cnt_get(sm.tcnt, src) == 0) {
-            const uint32_t b = sm.tbl[tbl_idx(p, nr, nc)];
-            if (b != CELL_CROWD) { iso = true; iso_ok = (b == 0) || ((L.ov >> b) & 1u); }
-        }
-        const int pr = L.r, pc = L.c;
-        bool moved = false;
-        if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)l; moved = true; }
-        bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
-#ifdef GW_STAMPS
-        {
-            const int nser = __popcll(__ballot(real && !iso)), nreal = __popcll(__ballot(real));
-            if (l == 0 && p.stamps) { p.stamps[(size_t)e * 32 + 30] = nser; p.stamps[(size_t)e * 32 + 31] = nreal; }
-        }
-#endif
-        STAMP(11);
-        for (uint64_t it = __ballot(real && !iso); it; it &= it - 1) {
-            const int a = first_lane(it);
-            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
-            if (l == a) { fail = !ok; moved = ok; }
-        }
-        if (fail) L.reward -= 0.1;
-        ctr += (uint32_t)WAVE;
-        // ---- entropy (:58-59)
-        if (acting) L.reward -= 0.01;
-        // cell table after the moves
-        wave_sync();
-        if (moved) {
-            const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
-            atomicSub(&sm.cnt[cnt_word(p, oc)], 1u << (8 * (oc & 3)));
-            atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
-            sm.tbl[tbl_idx(p, pr, pc)] = 0;
-        }
-        wave_sync();
-        if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
-        wave_sync();
-    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
-        // ---- attack pass (reach_the_target.py:96-108): every acting agent,
-        // dict order; only AttackingAgents attack (others return False, [])
-        const int32_t* act_e = p.actions + (size_t)e * A * p.act_dim;
-        for (uint64_t it = __ballot(acting && (L.kind & GW_K_ATTACKING)); it; it &= it - 1) {
-            const int a = first_lane(it);
-            if (!rlb(L.active, a)) continue;
-            int nlist, list;
-            const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
-                ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
-                : attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
-            if (!status) continue;
-            if (nlist == 0) { if (l == a) L.reward -= 0.1; }
-            else {
-                for (int t = 0; t < nlist; t++) {
-                    const int b = rl(list, t);
-                    if (!rlb(L.active, b)) {
-                        if (l == b) L.reward -= 1.0;
-                        if (l == a) L.reward += 1.0;
+                if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
+                STAMP(2);
+                // ---- move pass (:50-55)
+                const bool mover = acting && L.active;
+                const bool can_move = mover && (L.kind & GW_K_MOVING);
+                const int nr = L.r + mr, nc = L.c + mc;
+                const bool inb = 0 <= nr && nr < p.H && 0 <= nc && nc < p.W;
+                const bool stay = nr == L.r && nc == L.c;
+                const bool real = can_move && inb && !stay;
+                // isolation: no other mover targets my source or target, none leaves my target
+                const int HW = p.H * p.W;
+                const int nw = (HW + 3) / 4;
+                for (int i = l; i < nw; i += WAVE) { sm.tcnt[i] = 0u; sm.scnt[i] = 0u; }
+                wave_sync();
+                const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
+                if (real) {
+                    atomicAdd(&sm.tcnt[cnt_word(p, tgt)], 1u << (8 * (tgt & 3)));
+                    atomicAdd(&sm.scnt[cnt_word(p, src)], 1u << (8 * (src & 3)));
+                }
+                wave_sync();
+                bool iso = false, iso_ok = false;
+                if (real && cnt_get(sm.tcnt, tgt) == 1 && cnt_get(sm.scnt, tgt) == 0 &&
+                    cnt_get(sm.tcnt, src) == 0) {
+                    const uint32_t b = sm.tbl[tbl_idx(p, nr, nc)];
+                    if (b != CELL_CROWD) { iso = true; iso_ok = (b == 0) || ((L.ov >> b) & 1u); }
+                }
+                const int pr = L.r, pc = L.c;
+                bool moved = false;
+                if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)l; moved = true; }
+                bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
+        #ifdef GW_STAMPS
+                {
+                    const int nser = __popcll(__ballot(real && !iso)), nreal = __popcll(__ballot(real));
+                    if (l == 0 && p.stamps) { p.stamps[(size_t)e * GW_STAMP_STRIDE + 30] = nser; p.stamps[(size_t)e * GW_STAMP_STRIDE + 31] = nreal; }
+                }
+        #endif
+                STAMP(11);
+                for (uint64_t it = __ballot(real && !iso); it; it &= it - 1) {
+                    const int a = first_lane(it);
+                    const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                    if (l == a) { fail = !ok; moved = ok; }
+                }
+                if (fail) L.reward -= 0.1;
+                ctr += (uint32_t)WAVE;
+                // ---- entropy (:58-59)
+                if (acting) L.reward -= 0.01;
+                // cell table after the moves
+                wave_sync();
+                if (moved) {
+                    const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
+                    atomicSub(&sm.cnt[cnt_word(p, oc)], 1u << (8 * (oc & 3)));
+                    atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
+                    sm.tbl[tbl_idx(p, pr, pc)] = 0;
+                }
+                wave_sync();
+                if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
+                wave_sync();
+            } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+                // ---- attack pass (reach_the_target.py:96-108): every acting agent,
+                // dict order; only AttackingAgents attack (others return False, [])
+                const int32_t* act_e = act_t + (size_t)e * A * p.act_dim;
+                for (uint64_t it = __ballot(acting && (L.kind & GW_K_ATTACKING)); it; it &= it - 1) {
+                    const int a = first_lane(it);
+                    if (!rlb(L.active, a)) continue;
+                    int nlist, list;
+                    const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
+                        ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
+                        : attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                    if (!status) continue;
+                    if (nlist == 0) { if (l == a) L.reward -= 0.1; }
+                    else {
+                        for (int t = 0; t < nlist; t++) {
+                            const int b = rl(list, t);
+                            if (!rlb(L.active, b)) {
+                                if (l == b) L.reward -= 1.0;
+                                if (l == a) L.reward += 1.0;
+                            }
+                        }
                     }
                 }
-            }
-        }
-        STAMP(2);
-        // ---- move pass (:110-121): MovingAgents in dict order; active ones
-        // move (-0.1 on failure); then any of them on the target's cell is
-        // rewarded, removed from the grid and deactivated.  Removing one the
-        // target already killed there is the reference's KeyError.
-        const int t = p.target;
-        const int tr = rl(L.r, t), tc = rl(L.c, t);         // the target never moves
-        for (uint64_t it = __ballot(acting && (L.kind & GW_K_MOVING)); it; it &= it - 1) {
-            const int a = first_lane(it);
-            if (rlb(L.active, a)) {
-                const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
-                if (!ok && l == a) L.reward -= 0.1;
-            }
-            if (rl(L.r, a) == tr && rl(L.c, a) == tc) {
-                if (!rlb(L.in_grid, a)) {
-                    // Grid.remove raises KeyError: the step stops here (no
-                    // further moves, no observation draws); the env needs a
-                    // reset, which the auto-reset modes do as for an ended
-                    // episode (all_done set; SAME_STEP resets it right away)
-                    if (l == 0) {
-                        if (p.err) p.err[e] |= GW_ERR_DOUBLE_REMOVE;
-                        p.steps[e] = steps0 + 1;
-                        if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
-                        if (p.autoreset) p.all_done[e] = 1;
+                STAMP(2);
+                // ---- move pass (:110-121): MovingAgents in dict order; active ones
+                // move (-0.1 on failure); then any of them on the target's cell is
+                // rewarded, removed from the grid and deactivated.  Removing one the
+                // target already killed there is the reference's KeyError.
+                const int t = p.target;
+                const int tr = rl(L.r, t), tc = rl(L.c, t);         // the target never moves
+                for (uint64_t it = __ballot(acting && (L.kind & GW_K_MOVING)); it && !raised; it &= it - 1) {
+                    const int a = first_lane(it);
+                    if (rlb(L.active, a)) {
+                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                        if (!ok && l == a) L.reward -= 0.1;
                     }
+                    if (rl(L.r, a) == tr && rl(L.c, a) == tc) {
+                        if (!rlb(L.in_grid, a)) {
+                            // Grid.remove raises KeyError: the step stops here (no
+                            // further moves, no observation draws); the env needs a
+                            // reset, which the auto-reset modes do as for an ended
+                            // episode (all_done set; SAME_STEP resets it right away)
+                            raised = true;
+                            continue;
+                        }
+                        if (l == a) {
+                            L.reward += 1.0;
+                            L.in_grid = false;
+                            L.active = false;
+                        }
+                    }
+                }
+                ctr += (uint32_t)WAVE;
+                if (!raised) {
+                    // ---- entropy for the runners (:123-126)
+                    if (acting && (L.kind & GW_K_PROGRAM)) L.reward -= 0.01;
+                    // the LDS table after the passes (observation)
+                    build_tables(p, sm, L, true);
+                }
+            } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
+                const int n = p.nav, t = p.target;
+                if ((act_mask >> n) & 1) {
+                    const int pr = rl(L.r, n), pc = rl(L.c, n);
+                    const bool ok = move_one(p, L, n, rl(mr, n), rl(mc, n), ctr + (uint32_t)n);
+                    if (!ok && l == n) L.reward -= 0.1;
+                    const bool at = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+                    if (at && l == n) L.reward += 1.0;
+                    if (l == n) L.reward -= 0.01;
                     ctr += (uint32_t)WAVE;
-                    if (p.autoreset == 1) {
-                        // the table is not the post-move grid: rebuild from the template
+                    const int qr = rl(L.r, n), qc = rl(L.c, n);
+                    if (ok && (qr != pr || qc != pc)) {
+                        table_remove(p, sm, L, n, pr, pc);
+                        const int ncl = qr * p.W + qc;
+                        if (l == n) atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
                         wave_sync();
-                        reset_env<S>(p, e, sm, rng, L, ctr, false);
+                        if (L.in_grid && L.r == qr && L.c == qc)
+                            sm.tbl[tbl_idx(p, qr, qc)] = cell_byte(cnt_get(sm.cnt, ncl), L.enc);
+                        wave_sync();
                     }
-                    store_lane(p, e, L, valid);
-                    store_rng(p, e, sm, rng, ctr);
-                    return;
-                }
-                if (l == a) {
-                    L.reward += 1.0;
-                    L.in_grid = false;
-                    L.active = false;
                 }
             }
-        }
-        ctr += (uint32_t)WAVE;
-        // ---- entropy for the runners (:123-126)
-        if (acting && (L.kind & GW_K_PROGRAM)) L.reward -= 0.01;
-        // the LDS table after the passes (observation)
-        build_tables(p, sm, L, true);
-    } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        const int n = p.nav, t = p.target;
-        if ((act_mask >> n) & 1) {
-            const int pr = rl(L.r, n), pc = rl(L.c, n);
-            const bool ok = move_one(p, L, n, rl(mr, n), rl(mc, n), ctr + (uint32_t)n);
-            if (!ok && l == n) L.reward -= 0.1;
-            const bool at = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
-            if (at && l == n) L.reward += 1.0;
-            if (l == n) L.reward -= 0.01;
-            ctr += (uint32_t)WAVE;
-            const int qr = rl(L.r, n), qc = rl(L.c, n);
-            if (ok && (qr != pr || qc != pc)) {
-                table_remove(p, sm, L, n, pr, pc);
-                const int ncl = qr * p.W + qc;
-                if (l == n) atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
-                wave_sync();
-                if (L.in_grid && L.r == qr && L.c == qc)
-                    sm.tbl[tbl_idx(p, qr, qc)] = cell_byte(cnt_get(sm.cnt, ncl), L.enc);
-                wave_sync();
+            STAMP(3);
+            if (raised) {
+                // Grid.remove raised KeyError: the step stops here (no further
+                // moves, no observation draws, its outputs are not written); the
+                // env needs a reset, which the auto-reset modes do as for an
+                // ended episode (all_done set; SAME_STEP resets it right away)
+                if (l == 0 && p.err) p.err[e] |= GW_ERR_DOUBLE_REMOVE;
+                steps += 1;
+                acting_sum += (uint64_t)__popcll(act_mask);
+                if (p.autoreset && l == 0) ad_t[e] = 1;
+                prev_all = true;
+                // the table is not the post-move grid: from the template
+                if (p.autoreset == 1) { table_template(p, sm); reset_now = true; }
+                else need_tmpl = true;
+            } else {
+
+                // ---- observations of the live agents (all_step_manager.py:68-71)
+                STAMP(4);
+                observe_all<S>(p, e, sm, rng, L, obs_t);
+                STAMP(5);
+
+                // ---- rewards, dones (:72-79, smart.py:101-111)
+                bool dn;
+                bool only_left = false;                 // OnlyAgentLeftDone (reach_the_target.py:41-55)
+                if (p.sim_kind == GW_SIM_MAZE_NAV) {
+                    const int n = p.nav, t = p.target;
+                    dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
+                } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+                    const int t = p.target;
+                    const bool is_agent = (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
+                    only_left = __popcll(__ballot(valid && is_agent && L.active)) <= 1;
+                    const bool at_target = L.r == rl(L.r, t) && L.c == rl(L.c, t);
+                    // runners: ActiveDone or TargetDone; the target: OnlyAgentLeftDone (:144-150)
+                    dn = (L.kind & GW_K_PROGRAM) ? (!L.active || at_target) : only_left;
+                } else {
+                    dn = !L.active;
+                }
+                if (valid) {
+                    size_t k = (size_t)e * A + l;
+                    rew_t[k] = L.live ? L.reward : 0.0;
+                    done_t[k] = L.live ? (uint8_t)dn : (uint8_t)1;
+                }
+                const bool live_after = valid && L.live && !dn;
+                // get_all_done (done.py:49-56,147-153) or maze target reached
+                bool all;
+                if (p.sim_kind == GW_SIM_MAZE_NAV) {
+                    all = dn;
+                } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+                    all = only_left;
+                } else {
+                    all = true;
+                    // static entities are agents too, always active (done.py:49-56,147-153)
+                    if (p.done_kind & GW_DONE_ACTIVE) all = all && p.static_encs == 0 && (__ballot(valid && L.active) == 0);
+                    if (p.done_kind & GW_DONE_ONE_TEAM) {
+                        uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u) | p.static_encs;
+                        all = all && (__popc(bits) <= 1);
+                    }
+                }
+                const bool any_left = __ballot(live_after) != 0;
+                L.live = live_after;
+                const bool all_done = all || !any_left;
+                steps += 1;
+                acting_sum += (uint64_t)__popcll(act_mask);
+                if (l == 0) ad_t[e] = (uint8_t)all_done;
+                prev_all = all_done;
+                // SAME_STEP auto-reset: the next episode's first observation replaces obs
+                reset_now = p.autoreset == 1 && (all_done || (p.horizon > 0 && steps >= p.horizon));
             }
         }
-    }
-    STAMP(3);
-
-    // ---- observations of the live agents (all_step_manager.py:68-71)
-    STAMP(4);
-    observe_all<S>(p, e, sm, rng, L);
-    STAMP(5);
-
-    // ---- rewards, dones (:72-79, smart.py:101-111)
-    bool dn;
-    bool only_left = false;                 // OnlyAgentLeftDone (reach_the_target.py:41-55)
-    if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        const int n = p.nav, t = p.target;
-        dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
-    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
-        const int t = p.target;
-        const bool is_agent = (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
-        only_left = __popcll(__ballot(valid && is_agent && L.active)) <= 1;
-        const bool at_target = L.r == rl(L.r, t) && L.c == rl(L.c, t);
-        // runners: ActiveDone or TargetDone; the target: OnlyAgentLeftDone (:144-150)
-        dn = (L.kind & GW_K_PROGRAM) ? (!L.active || at_target) : only_left;
-    } else {
-        dn = !L.active;
-    }
-    if (valid) {
-        size_t k = (size_t)e * A + l;
-        p.reward[k] = L.live ? L.reward : 0.0;
-        p.done[k] = L.live ? (uint8_t)dn : (uint8_t)1;
-    }
-    const bool live_after = valid && L.live && !dn;
-    // get_all_done (done.py:49-56,147-153) or maze target reached
-    bool all;
-    if (p.sim_kind == GW_SIM_MAZE_NAV) {
-        all = dn;
-    } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
-        all = only_left;
-    } else {
-        all = true;
-        // static entities are agents too, always active (done.py:49-56,147-153)
-        if (p.done_kind & GW_DONE_ACTIVE) all = all && p.static_encs == 0 && (__ballot(valid && L.active) == 0);
-        if (p.done_kind & GW_DONE_ONE_TEAM) {
-            uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u) | p.static_encs;
-            all = all && (__popc(bits) <= 1);
+        if (reset_now) {
+            // the reset is the launch's critical path: issue it ahead of the
+            // SIMD's stepping waves
+            __builtin_amdgcn_s_setprio(3);
+            wave_sync();
+            STAMP(12);
+            reset_env<S>(p, e, sm, rng, L, ctr, true, obs_t);
+            STAMP(14);
+            steps = 0;
+            lanes_in = true;
+            if (next_reset) {
+                if (valid) {
+                    const size_t k = (size_t)e * A + l;
+                    rew_t[k] = 0.0;
+                    done_t[k] = L.live ? (uint8_t)0 : (uint8_t)1;
+                }
+                if (l == 0) ad_t[e] = 0;
+                prev_all = false;
+            }
+            __builtin_amdgcn_s_setprio(0);
         }
     }
-    const bool any_left = __ballot(live_after) != 0;
-    L.live = live_after;
-    const bool all_done = all || !any_left;
-    const int32_t steps = steps0 + 1;
     if (l == 0) {
-        p.all_done[e] = (uint8_t)all_done;
         p.steps[e] = steps;
-        if (p.acting) p.acting[e] = acting0 + (uint64_t)__popcll(act_mask);
-    }
-    // ---- SAME_STEP auto-reset: the next episode's first observation replaces obs
-    if (p.autoreset == 1 && (all_done || (p.horizon > 0 && steps >= p.horizon))) {
-        __builtin_amdgcn_s_setprio(3);                      // the launch's critical path
-        wave_sync();
-        STAMP(12);
-        reset_env<S>(p, e, sm, rng, L, ctr, true);
-        STAMP(14);
+        if (p.acting) p.acting[e] = acting_raw + acting_sum;
     }
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
@@ -2009,7 +2088,8 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
     load_env(p, e, sm, rng, ctr, false);
     ctr = 0;
     if (l == 0 && p.err) p.err[e] = 0u;     // an explicit reset starts the env's flags afresh
-    reset_env<S>(p, e, sm, rng, L, ctr, false);
+    reset_env<S>(p, e, sm, rng, L, ctr, false, p.obs);
+    if (l == 0) p.steps[e] = 0;
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
 }
@@ -2710,6 +2790,7 @@ gw_status gw_step(gw_handle g, const int32_t* actions, int32_t* obs, double* rew
     p.acting = acting;
     p.err = err_flags;
     p.autoreset = 0;
+    p.nsteps = 1; p.ad_in = all_done;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
     return GW_OK;
 }
@@ -2725,6 +2806,7 @@ gw_status gw_step_autoreset(gw_handle g, const int32_t* actions, int32_t* obs, d
     p.autoreset = 1;
     p.horizon = horizon;
     p.err = err_flags;
+    p.nsteps = 1; p.ad_in = all_done;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
     return GW_OK;
 }
@@ -2740,6 +2822,7 @@ gw_status gw_step_autoreset_next(gw_handle g, const int32_t* actions, int32_t* o
     p.autoreset = 2;
     p.horizon = horizon;
     p.err = err_flags;
+    p.nsteps = 1; p.ad_in = all_done;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
     return GW_OK;
 }
@@ -2915,7 +2998,49 @@ gw_status gw_rollout_step(gw_handle g, uint64_t key, uint32_t step, uint32_t env
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
+    p.nsteps = 1; p.ad_in = all_done;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
+                     uint8_t* done, uint8_t* all_done, const uint8_t* all_done_in, uint64_t* acting,
+                     int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
+                     void* stream)
+{
+    if (!g || n_steps <= 0 || !actions || !obs || !reward || !done || !all_done ||
+        autoreset < 1 || autoreset > 2)
+        return GW_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    Params p = g->base;
+    p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
+    p.persistent_obs = 0;                  // every step has its own obs slab
+    if (!g->wg && !g->pacman) {
+        // one launch: each env runs its n_steps back to back (step_kernel)
+        p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+        p.nsteps = n_steps; p.ad_in = all_done_in; p.skip_done_obs = skip_done_obs != 0;
+        HIPCHK(do_step(g, p, st));
+        return GW_OK;
+    }
+    // the workgroup and Pacman kernels: one launch per step, __all__ carried
+    // from slab t-1 to slab t (their all_done is in/out)
+    const size_t EA = (size_t)g->E * g->A;
+    int32_t orows, ocols;
+    gw_obs_shape(g, &orows, &ocols);
+    const size_t obs_stride = EA * (size_t)orows * ocols;
+    for (int t = 0; t < n_steps; t++) {
+        uint8_t* ad_t = all_done + (size_t)t * g->E;
+        const uint8_t* ad_prev = t == 0 ? all_done_in : all_done + (size_t)(t - 1) * g->E;
+        if (ad_prev) HIPCHK(hipMemcpyAsync(ad_t, ad_prev, (size_t)g->E, hipMemcpyDeviceToDevice, st));
+        else HIPCHK(hipMemsetAsync(ad_t, 0, (size_t)g->E, st));
+        p.actions = actions + (size_t)t * EA * p.act_dim;
+        p.obs = obs + (size_t)t * obs_stride;
+        p.reward = reward + (size_t)t * EA;
+        p.done = done + (size_t)t * EA;
+        p.all_done = ad_t;
+        p.nsteps = 1; p.ad_in = ad_t;
+        HIPCHK(do_step(g, p, st));
+    }
     return GW_OK;
 }
 

@@ -75,7 +75,7 @@ class GridWorldEngine:
         self.stamps = None
         if _native.VARIANT == 'stamps':
             # per-env s_memtime per phase (diagnostic build, tools/stamps.py)
-            self.stamps = torch.zeros((E, 32), dtype=torch.int64, device=dev)
+            self.stamps = torch.zeros((E, 64), dtype=torch.int64, device=dev)
             self.L.gw_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
             self.L.gw_debug_set_stamps(self.h, _ptr(self.stamps))
         if _native.VARIANT == 'checks':
@@ -241,6 +241,38 @@ class GridWorldEngine:
         return out
 
     AUTORESET_MODES = {'none': 0, 'same_step': 1, 'next_step': 2}
+
+    def rollout_buffers(self, n_steps):
+        """Per-step output slabs for rollout(): obs[n][E][A][...], reward[n][E][A],
+        done[n][E][A], all_done[n][E]."""
+        E, A, dev = self.E, self.A, self.device
+        return dict(obs=torch.empty((n_steps, E, A) + self.obs_shape, dtype=torch.int32, device=dev),
+                    reward=torch.empty((n_steps, E, A), dtype=torch.float64, device=dev),
+                    done=torch.empty((n_steps, E, A), dtype=torch.uint8, device=dev),
+                    all_done=torch.empty((n_steps, E), dtype=torch.uint8, device=dev))
+
+    def rollout(self, actions, horizon=0, autoreset='next_step', skip_done_obs=False, out=None):
+        """A fragment of K = actions.shape[0] consecutive steps with auto-reset
+        in ONE launch (gw_rollout): the results of K step_autoreset[_next]
+        calls with actions[t], written to per-step slabs (returned dict, or
+        `out` from rollout_buffers).  The '__all__' before step 0 is
+        self.all_done (the previous call's); afterwards self.all_done holds
+        the last step's.  skip_done_obs: obs rows of entities without an
+        observation in a step are left unwritten (mask them with done)."""
+        K = int(actions.shape[0])
+        assert actions.dtype == torch.int32 and actions.is_contiguous()
+        assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
+        assert autoreset in ('same_step', 'next_step'), autoreset
+        out = self.rollout_buffers(K) if out is None else out
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_rollout(
+                self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
+                self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream()),
+                'gw_rollout')
+            self.all_done.copy_(out['all_done'][K - 1])
+        self._check_debug('gw_rollout')
+        return out
 
     def rollout_step(self, key, step, env_offset=0, horizon=0, autoreset='next_step'):
         """One synthetic random-policy rollout step in ONE C-ABI call

@@ -291,6 +291,30 @@ gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
 gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
                             int32_t* actions, void* stream);
 
+/* A fragment of n_steps consecutive AllStepManager steps with auto-reset
+   (1 SAME_STEP, 2 NEXT_STEP) in one call: the same results as n_steps
+   calls of gw_step_autoreset / gw_step_autoreset_next with actions[t], but
+   the one-wave kernel runs each env's steps back to back in ONE launch (no
+   launch-wide barrier between steps; lane state, RNG and cell table stay on
+   chip).  Per-step slabs:
+     actions     device int32[n][E][A][gw_act_dim(h)]   (inputs, resident)
+     obs         device int32[n][E][A][obs shape]
+     reward      device double[n][E][A];  done  device uint8[n][E][A]
+     all_done    device uint8[n][E]       ('__all__' of every step)
+     all_done_in device uint8[E] or NULL  (the '__all__' before step 0, e.g.
+                 slab n-1 of the previous fragment; NULL = none set)
+     acting      device uint64[E] or NULL (+= acting agents over the steps)
+   skip_done_obs = 1: obs rows of entities that get no observation in a
+   step (done before it, or not grid observers) are left unwritten in that
+   step's slab instead of being filled with -2 (the reference returns no obs
+   for them; mask with done).  The workgroup-per-env and Pacman kernels run
+   the fragment as n_steps launches (same results, rows always written).
+   The handle's persistent obs rows (gw_config.persistent_obs) are not used. */
+gw_status gw_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
+                     uint8_t* done, uint8_t* all_done, const uint8_t* all_done_in, uint64_t* acting,
+                     int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
+                     void* stream);
+
 /* One step of a synthetic random-policy rollout in one call: gw_random_actions
    into `actions`, then on the same stream gw_step (autoreset 0),
    gw_step_autoreset (1) or gw_step_autoreset_next (2) on those actions.  The

@@ -44,9 +44,29 @@ for t in range(K):
     evs[t][0].record(); eng.step_autoreset_next(horizon=H); evs[t][1].record()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(json.dumps({'lib': %(lib)r, 'ms_per_step': dt / K * 1e3,
-                  'kernel_ms': float(np.mean([a.elapsed_time(b) for a, b in evs])),
-                  'agent_steps_per_s': (int(eng.acting.sum().item()) - a0) / dt}))
+res = {'lib': %(lib)r, 'ms_per_step': dt / K * 1e3,
+       'kernel_ms': float(np.mean([a.elapsed_time(b) for a, b in evs])),
+       'agent_steps_per_s': (int(eng.acting.sum().item()) - a0) / dt}
+if hasattr(L, 'gw_rollout'):
+    # the same steps continued as fragments of F steps, one launch each
+    for F in (20, 100):
+        acts = torch.empty((F,) + tuple(eng.actions.shape), dtype=torch.int32, device=eng.device)
+        out = eng.rollout_buffers(F)
+        for skip in (False, True):
+            best = None
+            for rep in range(3):
+                for s in range(F):
+                    eng.random_actions(9, 100000 + rep * F + s, out=acts[s])
+                torch.cuda.synchronize()
+                a0 = int(eng.acting.sum().item())
+                t0 = time.perf_counter()
+                eng.rollout(acts, horizon=H, skip_done_obs=skip, out=out)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                r = ((int(eng.acting.sum().item()) - a0) / dt, dt / F * 1e3)
+                best = r if best is None or r[0] > best[0] else best
+            res[f'rollout{F}{"_skip" if skip else ""}'] = {'agent_steps_per_s': best[0], 'ms_per_step': best[1]}
+print(json.dumps(res))
 '''
 
 for lib in sys.argv[1:]:

@@ -88,6 +88,11 @@ def main():
         if (~stepped).any():
             report(st[~stepped], [0, 10, 12, 11, 15, 13, 26, 27, 14, 6], TB_NEXT,
                    f'{wl}: resetting envs ({(~stepped).sum()})')
+        rs = st[~stepped]
+        print('health: rng.pos at start', rs[:, 40].tolist(), 'nrand', rs[:, 41].tolist())
+        for k, nm in enumerate(['word buffer', 'list lengths', 'draw offsets', 'rank+fixpoint', 'final']):
+            print(f'   jacobi {nm:>14}: median {np.median(rs[:, 20 + k]):8.0f} max {rs[:, 20 + k].max():8.0f}')
+        print(f'   jacobi sweeps: median {np.median(rs[:, 25]):.0f} max {rs[:, 25].max()}')
         tot = st[:, 6] - st[:, 0]
         print(f'launch span (last end - first start, if the counter is global): '
               f'{st[:, 6].max() - st[:, 0].min()} ticks; starts spread over {st[:, 0].max() - st[:, 0].min()}')
