@@ -453,10 +453,12 @@ struct Smem {
 // Jacobi placement scratch in the work area (do_reset): stream words,
 // per-lane (fresh, enc), chunk prefix counts, lane bits by cell rank, their
 // prefix ORs, and a twisted copy of the key
-constexpr int JAC_WB = 192;
+// (sized so that the TeamBattle 32x32 env fits 10 KiB of LDS: 16 one-wave
+// envs per CU, all 4096 resident at once on 256 CUs)
+constexpr int JAC_WB = 160;
 constexpr int JAC_OFF_W = 0;
 constexpr int JAC_OFF_PUB = JAC_OFF_W + 4 * JAC_WB;
-constexpr int JAC_OFF_CP = JAC_OFF_PUB + 8 * 64;
+constexpr int JAC_OFF_CP = JAC_OFF_PUB + 4 * 64;
 constexpr int JAC_OFF_SB = JAC_OFF_CP + 4 * 64;
 constexpr int JAC_OFF_T = JAC_OFF_SB + 8 * 64;
 constexpr int JAC_OFF_KEY2 = JAC_OFF_T + 8 * 64;
@@ -615,6 +617,84 @@ __device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const La
 // SP = 4*ceil(S/4) bytes so a decoded table dword is written to LDS as is.
 __host__ __device__ constexpr int stage_pitch(int S) { return (S + 3) & ~3; }
 
+// Lane l's row-padded stage rows [S][SP] -> SS consecutive bytes at byte
+// l*SS of the stage (in place; lanes >= A untouched).  Byte i of the row
+// stream is window row i / S, column i % S.
+template <int S>
+__device__ __forceinline__ void compact_stage(Smem& sm, int A)
+{
+    constexpr int NW = (S + 3) / 4;
+    constexpr int SSP = S * stage_pitch(S);
+    constexpr int SS = S * S;
+    constexpr int CW = (SS + 3) / 4;            // stream dwords
+    const int l = lane_id();
+    uint32_t rw[S * NW];
+    const uint32_t* st32 = (const uint32_t*)sm.stage;
+#pragma unroll
+    for (int k = 0; k < S * NW; k++) rw[k] = l < A ? st32[l * (SSP / 4) + k] : 0u;
+    wave_sync();
+    if (l < A) {
+        uint32_t seg[CW];
+#pragma unroll
+        for (int g = 0; g < CW; g++) {
+            // stream bytes 4g..4g+3 from at most two row dwords (one perm), or
+            // assembled byte by byte when they span three
+            int src[4], sb[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int i = 4 * g + b < SS ? 4 * g + b : SS - 1;
+                const int r = i / S, c = i % S;
+                src[b] = r * NW + (c >> 2);
+                sb[b] = c & 3;
+            }
+            const int s0 = src[0];
+            int s1 = s0;
+#pragma unroll
+            for (int b = 1; b < 4; b++) if (src[b] != s0) s1 = src[b];
+            bool two = true;
+#pragma unroll
+            for (int b = 0; b < 4; b++) two = two && (src[b] == s0 || src[b] == s1);
+            if (two) {
+                // v_perm_b32(hi, lo, sel): selector byte k picks byte k of lo
+                // (0-3) or of hi (4-7)
+                uint32_t sel = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) sel |= (uint32_t)((src[b] == s0 ? 0 : 4) + sb[b]) << (8 * b);
+                seg[g] = __builtin_amdgcn_perm(rw[s1], rw[s0], sel);
+            } else {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) v |= ((rw[src[b]] >> (8 * sb[b])) & 0xffu) << (8 * b);
+                seg[g] = v;
+            }
+        }
+        // memory dword k of this lane's span holds stream bytes [4k - s, 4k - s + 4)
+        const int s = (l * SS) & 3;
+        uint32_t* dst = (uint32_t*)sm.stage + ((l * SS) >> 2);
+#pragma unroll
+        for (int k = 0; k <= CW; k++) {
+            const uint32_t lo_w = k == 0 ? 0u : seg[k - 1];
+            const uint32_t hi_w = k < CW ? seg[k] : 0u;
+            const uint32_t val = (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (32 - 8 * s));
+            if (k >= 1 && 4 * k + 4 <= SS) {            // full for every s
+                dst[k] = val;
+            } else {
+                const int lo = k == 0 ? s : 0;
+                const int hi = s + SS - 4 * k < 4 ? s + SS - 4 * k : 4;
+                if (lo == 0 && hi == 4) {
+                    dst[k] = val;
+                } else {
+                    uint8_t* d8 = (uint8_t*)(dst + k);
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        if (b >= lo && b < hi) d8[b] = (uint8_t)(val >> (8 * b));
+                }
+            }
+        }
+    }
+    wave_sync();
+}
+
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S>
 __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
@@ -714,8 +794,10 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             else stage_rows(std::integral_constant<bool, false>());
         } else {
             uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
+            // -2 rows; a row the store skips holds the 0x80 sentinel instead
+            const uint32_t fill = ((skip >> l) & 1ull) ? 0x80808080u : 0xFEFEFEFEu;
 #pragma unroll
-            for (int k = 0; k < S * NW; k++) st32[k] = 0xFEFEFEFEu;
+            for (int k = 0; k < S * NW; k++) st32[k] = fill;
         }
     }
     wave_sync();
@@ -864,49 +946,44 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     wave_sync();
     STAMP(stamp_base + 1);
 
-    // stage (int8) -> obs (int32), 4 consecutive values per lane (lane-
-    // contiguous int4 stores).  Output m sits at stage byte m + (m/S)(SP-S);
-    // when rows are padded by one byte (S = 7, 11, 15) four consecutive
-    // outputs lie within two stage dwords: one byte-permute.
+    // stage (int8) -> obs (int32).  First every lane compacts its own
+    // row-padded [S][SP] stage rows into SS consecutive bytes at l*SS (in
+    // place: all rows are read before any is written), so that output m is
+    // stage byte m; then lane-contiguous int4 stores of 4 consecutive
+    // outputs from one aligned stage dword each.  Rows the store skips hold
+    // the 0x80 sentinel: a dword of four sentinels is not stored, a mixed one
+    // stores -2 for them (max(v, -2): valid bytes are >= -2).
+    compact_stage<S>(sm, A);
     const int total = A * SS;
     int32_t* out = obs + (size_t)e * total;
-    if (S >= 4 && SP - S <= 1 && (total & 3) == 0) {
+    const uint32_t* cs = (const uint32_t*)sm.stage;
+    if ((total & 3) == 0) {
         constexpr int NIT = (GW_MAX_AGENTS * SS + 4 * WAVE - 1) / (4 * WAVE);
         constexpr int B = NIT < 7 ? NIT : 7;                    // LDS reads in flight
-        constexpr uint32_t GAP = SP - S;
         for (int k0 = 0; k0 < NIT && k0 * 4 * WAVE < total; k0 += B) {
-            uint32_t lo[B], hi[B], sel[B];
+            uint32_t w[B];
 #pragma unroll
             for (int k = 0; k < B; k++) {
                 const int m = ((k0 + k) * WAVE + l) * 4;
-                const int mm = m < total ? m : 0;
-                const int q0 = mm / S, wc0 = mm - q0 * S;
-                const int base = mm + q0 * (int)GAP;
-                const int t = S - wc0;                           // outputs left in this row
-                uint32_t sl = (uint32_t)(base & 3) * 0x01010101u + 0x03020100u;
-                if (t < 4) sl += (GAP * 0x01010101u) << (8 * t);
-                sel[k] = sl;
-                const uint32_t* src = (const uint32_t*)(sm.stage + (base & ~3));
-                lo[k] = src[0];
-                hi[k] = src[1];
+                w[k] = cs[(m < total ? m : 0) >> 2];
             }
 #pragma unroll
             for (int k = 0; k < B; k++) {
                 const int m = ((k0 + k) * WAVE + l) * 4;
-                // the four outputs belong to lanes m / SS and (m + 3) / SS
-                const bool keep = m < total &&
-                                  !((skip >> (m / SS)) & (skip >> ((m + 3) / SS)) & 1ull);
-                if (keep) {
-                    const uint32_t w = __builtin_amdgcn_perm(hi[k], lo[k], sel[k]);
-                    *(int4*)(out + m) = make_int4((int8_t)(w & 0xff), (int8_t)((w >> 8) & 0xff),
-                                                  (int8_t)((w >> 16) & 0xff), (int8_t)(w >> 24));
+                if (m < total && (!skip || w[k] != 0x80808080u)) {
+                    int4 v = make_int4((int8_t)(w[k] & 0xff), (int8_t)((w[k] >> 8) & 0xff),
+                                       (int8_t)((w[k] >> 16) & 0xff), (int8_t)(w[k] >> 24));
+                    if (skip) {
+                        v.x = max(v.x, -2); v.y = max(v.y, -2); v.z = max(v.z, -2); v.w = max(v.w, -2);
+                    }
+                    *(int4*)(out + m) = v;
                 }
             }
         }
     } else {
         for (int m = l; m < total; m += WAVE) {
-            const int q = m / S;
-            if (!((skip >> (m / SS)) & 1ull)) out[m] = sm.stage[m + q * (SP - S)];
+            const int v = sm.stage[m];
+            if (!((skip >> (m / SS)) & 1ull)) out[m] = v < -2 ? -2 : v;
         }
     }
 }
@@ -1422,7 +1499,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const uint64_t before = ip ? (ipm & lt_l) : (rnd ? (ipm | (rndm & lt_l)) : 0ull);
         const uint32_t rem = valid ? (p.no_overlap_at_reset ? all_encs : (all_encs & ~L.ov)) : 0u;
         uint32_t* wbuf = (uint32_t*)(sm.stage + JAC_OFF_W);
-        uint2* pub = (uint2*)(sm.stage + JAC_OFF_PUB);
+        uint32_t* pub = (uint32_t*)(sm.stage + JAC_OFF_PUB);   // fresh | enc << 16
         uint32_t* cpa = (uint32_t*)(sm.stage + JAC_OFF_CP);
         uint2* sb = (uint2*)(sm.stage + JAC_OFF_SB);
         uint2* tb = (uint2*)(sm.stage + JAC_OFF_T);
@@ -1539,7 +1616,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             // rank this sweep's cell estimates
             const int ce0 = rnd ? (nidx != idx ? nidx : cell) : cell;
             for (int i = l; i < nw; i += WAVE) hist[i] = 0u;
-            if (valid) pub[l] = make_uint2(fresh, (uint32_t)L.enc);
+            if (valid) pub[l] = fresh | ((uint32_t)L.enc << 16);
             sb[l] = make_uint2(0u, 0u);
             wave_sync();
             uint32_t tie = 0;
@@ -1590,7 +1667,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             while (dm) {
                 const int j = __builtin_ctzll(dm);
                 dm &= dm - 1ull;
-                const uint2 pj = pub[j];
+                const uint32_t pw = pub[j];
+                const uint2 pj = make_uint2(pw & 0xffffu, pw >> 16);
                 dup |= pj.x;
                 qb |= !((L.ov >> pj.y) & 1u);
             }

@@ -80,6 +80,18 @@ def step_bytes(E, A, S):
     return E * (A * per_slot + per_env)
 
 
+def rollout_bytes(E, A, S, n_steps, acting, act_dim=3):
+    """Algorithmic HBM bytes of one gw_rollout launch of n_steps steps with
+    skip_done_obs (SURVEY §8d per agent-step, obs only for the agents that get
+    one): per step and entity slot actions 4*act_dim + reward 8 + done 1,
+    per step and env __all__ 1, obs 4*S*S per acting agent-step (`acting`
+    over the launch: every acting agent observes in these programs), and the
+    per-launch state read+write 2*(pos 8 + seq 4 + health 8 + flags 1) per
+    slot + 41 B per env (step / acting counters, RNG position)."""
+    return (n_steps * E * (A * (4 * act_dim + 8 + 1) + 1) + 4 * S * S * acting +
+            E * A * 2 * (8 + 4 + 8 + 1) + E * 41)
+
+
 def rtt_step_bytes(E, A, S, act_dim):
     """step_bytes with the SelectiveAttackActor's wider action rows
     (4 * act_dim B per entity slot instead of 12)."""
@@ -217,6 +229,13 @@ def main():
                     help='start every episode at step 0 (default: the first episode of global env '
                          'e starts at step e * horizon // envs, so horizon resets are spread over '
                          'the steps instead of all envs resetting together every horizon)')
+    ap.add_argument('--mode', choices=['rollout', 'step'], default='rollout',
+                    help="rollout (default): the timed steps run as gw_rollout fragments (one launch "
+                         "per --fragment steps, each env steps back to back inside it) on actions "
+                         "already in HBM; step: one launch per step (closed loop, the RLlib "
+                         "per-step protocol), with the Philox action kernel in the timed region")
+    ap.add_argument('--fragment', type=int, default=100,
+                    help='steps per gw_rollout launch (rollout mode)')
     ap.add_argument('--event-every', type=int, default=4,
                     help='HIP events around the step kernel of every n-th timed step (the others '
                          'go through the one-call gw_rollout_step path)')
@@ -253,7 +272,7 @@ def main():
     allow = _abi.GW_ERR_DOUBLE_REMOVE if args.workload == 'rtt' else 0
     untimed = args.preroll + args.warmup
 
-    def run(mode):
+    def run(mode, rollout):
         """Fresh engine (same seeds), pre-roll + warmup, then K timed steps."""
         eng = GridWorldEngine(cc, E_local, seeds=env_seeds(E_local, run=0, first_env=first))
         if turn:
@@ -273,6 +292,8 @@ def main():
         eng.check_errors()
         step = (lambda: eng.turn_step(horizon=args.horizon)) if turn else \
             (eng.step_autoreset_next if mode == 'next_step' else eng.step_autoreset)
+        if rollout:
+            return eng, run_rollout(eng, mode)
         for t in range(untimed):
             if turn:
                 eng.random_actions(key, t, env_offset=first)
@@ -322,22 +343,86 @@ def main():
             dist.all_reduce(kms, op=dist.ReduceOp.MAX)
             tot = torch.stack([acts[0], tmax[1], acts[2]])
         return eng, dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
-                         step_ms=step_ms, step_ms_max=kms[0].item())
+                         step_ms=step_ms, step_ms_max=kms[0].item(), steps_per_launch=1,
+                         acting_local=acting)
+
+    def run_rollout(eng, mode):
+        """Pre-roll and warmup as rollout fragments, then the K timed steps as
+        gw_rollout fragments of up to --fragment steps on actions generated
+        into HBM before the timed region; HIP events around every launch."""
+        F = max(1, min(args.fragment, args.steps))
+        acts = torch.empty((max(F, min(args.fragment, max(untimed, 1))),) + tuple(eng.actions.shape),
+                           dtype=torch.int32, device=eng.device)
+        out = eng.rollout_buffers(acts.shape[0])
+        t = 0
+        while t < untimed:                  # untimed pre-roll + warmup
+            f = min(acts.shape[0], untimed - t)
+            for s in range(f):
+                eng.random_actions(key, t + s, env_offset=first, out=acts[s])
+            eng.rollout(acts[:f], horizon=args.horizon, autoreset=mode, skip_done_obs=True, out=out)
+            t += f
+        torch.cuda.synchronize()
+        eng.check_errors(allow=allow)
+        # the timed steps' actions: inputs resident in HBM before timing
+        all_acts = torch.empty((args.steps,) + tuple(eng.actions.shape), dtype=torch.int32,
+                               device=eng.device)
+        for s in range(args.steps):
+            eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
+        frags = [(i, min(F, args.steps - i)) for i in range(0, args.steps, F)]
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in frags]
+        torch.cuda.synchronize()
+        acting0 = int(eng.acting.sum().item())
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for (i, f), ev in zip(frags, evs):
+            ev[0].record()
+            eng.rollout(all_acts[i:i + f], horizon=args.horizon, autoreset=mode, skip_done_obs=True,
+                        out=out)
+            ev[1].record()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        eng.check_errors(allow=allow)
+        acting = int(eng.acting.sum().item()) - acting0
+        # launch-weighted mean: ms per launch of the full-size fragments
+        full = [a.elapsed_time(b) for (i, f), (a, b) in zip(frags, evs) if f == F]
+        launch_ms = float(np.mean(full))
+        tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
+        kms = torch.tensor([launch_ms], dtype=torch.float64, device=eng.device)
+        if dist:
+            acts_t = tot.clone(); dist.all_reduce(acts_t, op=dist.ReduceOp.SUM)
+            tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(kms, op=dist.ReduceOp.MAX)
+            tot = torch.stack([acts_t[0], tmax[1], acts_t[2]])
+        return dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
+                    step_ms=launch_ms, step_ms_max=kms[0].item(), steps_per_launch=F,
+                    acting_local=acting)
 
     mode = 'next_step' if turn else args.autoreset
+    rollout = args.mode == 'rollout' and not turn
     other = 'same_step' if mode == 'next_step' else 'next_step'
-    eng, r = run(mode)
+    eng, r = run(mode, rollout)
     A, n_passive = eng.A, eng.n_passive
     stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
     del eng
-    r2 = None if (args.no_other or turn) else run(other)[1]
+    r2 = None if (args.no_other or turn) else run(other, rollout)[1]
+    # the per-step (closed-loop) protocol beside the rollout line
+    r3 = run(mode, False)[1] if (rollout and not args.no_other) else None
     acting_all, dt_all, envs_all = r['acting'], r['dt'], r['envs']
     step_ms_all = r['step_ms_max']
 
     if rank == 0:
         value = acting_all / dt_all
         S = cc.obs_side
-        if args.workload == 'team_battle' or args.workload == 'maze':
+        F = r['steps_per_launch']
+        if rollout:
+            # per launch: the local rank's acting agent-steps scaled to one launch
+            nbytes = rollout_bytes(E_local, A, S, F, r['acting_local'] * F / args.steps, cc.act_dim)
+        elif args.workload == 'team_battle' or args.workload == 'maze':
             nbytes = step_bytes(E_local, A, S)
         elif args.workload == 'rtt':
             nbytes = rtt_step_bytes(E_local, A, S, cc.act_dim)
@@ -345,12 +430,15 @@ def main():
             nbytes = pacman_turn_bytes(E_local, A, cc.rows * cc.cols, (n_passive + 31) // 32)
         scaling = 'strong' if strong else 'weak'
         workload = (f'{wdesc}, {E_local} envs per GPU ({int(envs_all)} in total, {scaling} scaling), '
-                    f'horizon {args.horizon}, {mode} auto-reset, {args.preroll}-step pre-roll')
+                    f'horizon {args.horizon}, {mode} auto-reset, {args.preroll}-step pre-roll, ' +
+                    (f'gw_rollout fragments of {F} steps on actions resident in HBM (one launch '
+                     f'per fragment, obs written for the agents that get one)' if rollout else
+                     'one step launch per step + the Philox action kernel'))
         if args.workload != 'team_battle':
             workload += ' (not the headline metric\'s config)'
         achieved = nbytes / (step_ms_all * 1e-3) / 1e9
         traffic, rocprof_ms = None, None
-        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}.json')
+        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{"_rollout" if rollout else ""}.json')
         if args.workload == 'team_battle' and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')
@@ -358,8 +446,11 @@ def main():
         roof = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                 'traffic': traffic, 'kernel': kname, 'kernel_ms': round(step_ms_all, 4),
-                'kernel_timing': f'HIP events around the step kernel of every {max(1, args.event_every)}'
-                                 f'-th timed step (launch stream), mean; max over ranks',
+                'kernel_timing': (f'HIP events around every gw_rollout launch ({F} steps) on the launch '
+                                  f'stream, mean; max over ranks' if rollout else
+                                  f'HIP events around the step kernel of every {max(1, args.event_every)}'
+                                  f'-th timed step (launch stream), mean; max over ranks'),
+                'steps_per_launch': F,
                 'bytes_per_launch': nbytes}
         if rocprof_ms:
             # the same ratio with the committed rocprofv3 kernel-trace average
@@ -394,6 +485,12 @@ def main():
                 'mode': other, 'value': round(r2['acting'] / r2['dt'], 1),
                 'ms_per_step': round(r2['dt'] / args.steps * 1e3, 4),
                 'kernel_ms': round(r2['step_ms_max'], 4)},
+            'closed_loop': None if r3 is None else {
+                'protocol': 'one step launch per step (RLlib per-step protocol), Philox action '
+                            'kernel in the timed region, HIP events on every 4th step kernel',
+                'value': round(r3['acting'] / r3['dt'], 1),
+                'ms_per_step': round(r3['dt'] / args.steps * 1e3, 4),
+                'kernel_ms': round(r3['step_ms_max'], 4)},
         }
         if world == 1 and not args.no_other and args.workload == 'team_battle':
             # BASELINE configs 2, 4 and 5 (single GPU, short runs; not the metric)
