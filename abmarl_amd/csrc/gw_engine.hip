@@ -154,7 +154,16 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
+// The lane id through a volatile asm: the step loop (gw_rollout) would
+// otherwise let the compiler hoist every lane-derived address and mask out of
+// the loop and keep them live in VGPRs across all of it (179 VGPRs and
+// scratch spills instead of 124).  Recomputing it costs two VALU per use.
+__device__ __forceinline__ int lane_id()
+{
+    int v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+}
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
