@@ -41,6 +41,7 @@ GW_SIM_TEAM_BATTLE = 1
 GW_SIM_MAZE_NAV = 2
 GW_SIM_REACH_TARGET = 3
 GW_SIM_PACMAN = 4
+GW_SIM_TRAFFIC = 5
 
 GW_OBS_POSITION_CENTERED = 0
 GW_OBS_ABSOLUTE = 1
@@ -50,6 +51,8 @@ GW_ATTACK_SELECTIVE = 1
 
 GW_DONE_ACTIVE = 0x1
 GW_DONE_ONE_TEAM = 0x2
+GW_DONE_TARGET_AGENT = 0x4
+GW_DONE_TARGET_DESTROYED = 0x8
 
 GW_ORDER_POSITION_HEALTH = 0
 GW_ORDER_HEALTH_POSITION = 1
@@ -75,7 +78,17 @@ class AgentSpec(C.Structure):
         ("attack_accuracy", C.c_double),
         ("initial_health", C.c_double),
         ("initial_orientation", C.c_int32),
+        ("done_target", C.c_int32),
+        ("destroy_target", C.c_int32),
     ]
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        # entity indices; -1 = not in the done component's target_mapping
+        if 'done_target' not in kwargs:
+            self.done_target = -1
+        if 'destroy_target' not in kwargs:
+            self.destroy_target = -1
 
 
 class Config(C.Structure):

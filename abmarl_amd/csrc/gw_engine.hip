@@ -71,6 +71,10 @@ struct DevAgent {               // per-entity constants (spec table in HBM)
     int32_t view_range, move_range, attack_range, simul;
     double strength, accuracy, init_health;
     int32_t init_orient;
+    // done components' targets (gw_agent_spec.done_target / destroy_target):
+    // the target's lane, -1 not mapped, -2 a static entity (at tgt_pos =
+    // row << 16 | col, always active)
+    int32_t tgt_lane, tgt_pos, dtgt_lane;
 };
 
 struct Params {
@@ -1323,6 +1327,81 @@ __device__ __forceinline__ void renorm_seq(const Params& p, Lane& L, uint32_t& c
     ctr = (uint32_t)p.A;
 }
 
+// ------------------------------------------------------------ done components
+// SmartGridWorldSimulation.get_done (smart.py:106-111): the AND of the done
+// components, all([]) = True.  ActiveDone / OneTeamRemainingDone: not active
+// (done.py:44-48); TargetAgentDone: on the target's position (np.array_equal,
+// done.py:91-95; a removed agent keeps its last position); TargetDestroyedDone:
+// the target is inactive (done.py:131-132).  Targets are read from the spec
+// table on demand (only the target programs pay for them).
+__device__ __forceinline__ void target_of(const Params& p, const Lane& L, int32_t& tl, int32_t& tpos,
+                                          int32_t& dl)
+{
+    const int l = lane_id();
+    const DevAgent* s = p.spec + (l < p.A ? l : 0);
+    tl = l < p.A ? s->tgt_lane : -1;
+    tpos = s->tgt_pos;
+    dl = l < p.A ? s->dtgt_lane : -1;
+}
+
+// this lane's get_done (every lane at once)
+__device__ __forceinline__ bool lane_done(const Params& p, const Lane& L)
+{
+    const uint32_t dk = p.done_kind;
+    bool d = true;
+    if (dk & (GW_DONE_ACTIVE | GW_DONE_ONE_TEAM)) d = d && !L.active;
+    if (dk & (GW_DONE_TARGET_AGENT | GW_DONE_TARGET_DESTROYED)) {
+        int32_t tl, tpos, dl;
+        target_of(p, L, tl, tpos, dl);
+        const int ti = tl >= 0 ? tl : lane_id(), di = dl >= 0 ? dl : lane_id();
+        const int tr = __shfl(L.r, ti), tc = __shfl(L.c, ti);
+        const bool da = __shfl((int)L.active, di) != 0;
+        if (dk & GW_DONE_TARGET_AGENT) {
+            const int rr = tl == -2 ? (tpos >> 16) : tr, cc = tl == -2 ? (tpos & 0xffff) : tc;
+            d = d && tl != -1 && L.r == rr && L.c == cc;
+        }
+        if (dk & GW_DONE_TARGET_DESTROYED) d = d && dl >= 0 && !da;   // a static target never dies
+    }
+    return d;
+}
+
+// get_done of lane a (uniform), at this point of the step
+__device__ __forceinline__ bool lane_done_uniform(const Params& p, const Lane& L, int a)
+{
+    const uint32_t dk = p.done_kind;
+    bool d = true;
+    if (dk & (GW_DONE_ACTIVE | GW_DONE_ONE_TEAM)) d = d && !rlb(L.active, a);
+    if (dk & (GW_DONE_TARGET_AGENT | GW_DONE_TARGET_DESTROYED)) {
+        const DevAgent* s = p.spec + a;
+        const int tl = uni(s->tgt_lane), tpos = uni(s->tgt_pos), dl = uni(s->dtgt_lane);
+        if (dk & GW_DONE_TARGET_AGENT) {
+            const int ar = rl(L.r, a), ac = rl(L.c, a);
+            const int tr = tl >= 0 ? rl(L.r, tl) : (tpos >> 16), tc = tl >= 0 ? rl(L.c, tl) : (tpos & 0xffff);
+            d = d && tl != -1 && ar == tr && ac == tc;
+        }
+        if (dk & GW_DONE_TARGET_DESTROYED) d = d && dl >= 0 && !rlb(L.active, dl);
+    }
+    return d;
+}
+
+// the target components' get_all_done: every MAPPED entity done (done.py:97-99,134-137)
+__device__ __forceinline__ bool targets_all_done(const Params& p, const Lane& L)
+{
+    const uint32_t dk = p.done_kind;
+    int32_t tl, tpos, dl;
+    target_of(p, L, tl, tpos, dl);
+    const int ti = tl >= 0 ? tl : lane_id(), di = dl >= 0 ? dl : lane_id();
+    const int tr = __shfl(L.r, ti), tc = __shfl(L.c, ti);
+    const bool da = __shfl((int)L.active, di) != 0;
+    bool bad = false;
+    if (dk & GW_DONE_TARGET_AGENT) {
+        const int rr = tl == -2 ? (tpos >> 16) : tr, cc = tl == -2 ? (tpos & 0xffff) : tc;
+        bad = bad || (tl != -1 && !(L.r == rr && L.c == cc));
+    }
+    if (dk & GW_DONE_TARGET_DESTROYED) bad = bad || (dl == -2 || (dl >= 0 && da));
+    return __ballot(lane_id() < p.A && bad) == 0;
+}
+
 // ------------------------------------------------------------ reset
 // AllStepManager.reset (all_step_manager.py:37-49) -> SmartGWS.reset ->
 // PositionState.reset (state.py:88-166) / HealthState.reset (:629-641) in the
@@ -2030,6 +2109,18 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     // the LDS table after the passes (observation)
                     build_tables(p, sm, L, true);
                 }
+            } else if (p.sim_kind == GW_SIM_TRAFFIC) {
+                // ---- traffic_corridor.py:41-49: the action dict in dict order;
+                // a failed move (None for non-MovingAgents) -0.1, then +1 when
+                // get_done(agent) holds right after the agent's own move
+                for (uint64_t it = act_mask; it; it &= it - 1) {
+                    const int a = first_lane(it);
+                    const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                    if (!ok && l == a) L.reward -= 0.1;
+                    if (lane_done_uniform(p, L, a) && l == a) L.reward += 1.0;
+                }
+                ctr += (uint32_t)WAVE;
+                build_tables(p, sm, L, true);       // the LDS table after the moves
             } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
                 const int n = p.nav, t = p.target;
                 if ((act_mask >> n) & 1) {
@@ -2087,7 +2178,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     // runners: ActiveDone or TargetDone; the target: OnlyAgentLeftDone (:144-150)
                     dn = (L.kind & GW_K_PROGRAM) ? (!L.active || at_target) : only_left;
                 } else {
-                    dn = !L.active;
+                    dn = lane_done(p, L);
                 }
                 if (valid) {
                     size_t k = (size_t)e * A + l;
@@ -2109,6 +2200,8 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                         uint32_t bits = wave_or((valid && L.active) ? (1u << L.enc) : 0u) | p.static_encs;
                         all = all && (__popc(bits) <= 1);
                     }
+                    if (p.done_kind & (GW_DONE_TARGET_AGENT | GW_DONE_TARGET_DESTROYED))
+                        all = all && targets_all_done(p, L);
                 }
                 const bool any_left = __ballot(live_after) != 0;
                 L.live = live_after;
@@ -2446,7 +2539,7 @@ static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 3; }
+int32_t gw_abi_version(void) { return 4; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
@@ -2466,7 +2559,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         return GW_E_UNSUPPORTED;
     }
     if (cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_MAZE_NAV &&
-        cfg->sim_kind != GW_SIM_REACH_TARGET && cfg->sim_kind != GW_SIM_PACMAN) {
+        cfg->sim_kind != GW_SIM_REACH_TARGET && cfg->sim_kind != GW_SIM_PACMAN &&
+        cfg->sim_kind != GW_SIM_TRAFFIC) {
         set_err("unknown sim_kind %d", cfg->sim_kind);
         return GW_E_INVALID;
     }
@@ -2620,11 +2714,42 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].strength = s.attack_strength; hs[l].accuracy = s.attack_accuracy;
         hs[l].init_health = s.initial_health;
         hs[l].init_orient = s.initial_orientation;
+        hs[l].tgt_lane = -1; hs[l].tgt_pos = 0; hs[l].dtgt_lane = -1;
     }
     for (int l = 0; l < GW_MAX_LANES; l++) {
         g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
                                   ((uint32_t)(hs[l].attack_range & 0xf) << 16) |
                                   ((uint32_t)(hs[l].simul & 0xfff) << 20)) : 0u;
+    }
+    // done components' targets (TargetAgentDone / TargetDestroyedDone)
+    {
+        const uint32_t tbits = GW_DONE_TARGET_AGENT | GW_DONE_TARGET_DESTROYED;
+        if ((cfg->done_kind & tbits) && cfg->sim_kind != GW_SIM_TEAM_BATTLE && cfg->sim_kind != GW_SIM_TRAFFIC) {
+            set_err("TargetAgentDone / TargetDestroyedDone run with the TeamBattle and traffic programs");
+            return GW_E_UNSUPPORTED;
+        }
+        std::vector<int> lane_of(NE, -1);
+        for (int l = 0; l < A; l++) lane_of[lanes[l]] = l;
+        for (int a = 0; a < NE; a++) {
+            const gw_agent_spec& s = cfg->agents[a];
+            if (s.done_target < -1 || s.done_target >= NE || s.destroy_target < -1 || s.destroy_target >= NE) {
+                set_err("agent %d: target index outside the entities", a);
+                return GW_E_INVALID;
+            }
+            if (lane_of[a] < 0 && (s.done_target >= 0 || s.destroy_target >= 0)) {
+                set_err("static entity %d as a target_mapping key", a);
+                return GW_E_UNSUPPORTED;
+            }
+        }
+        for (int l = 0; l < A; l++) {
+            const gw_agent_spec& s = cfg->agents[lanes[l]];
+            if (s.done_target >= 0) {
+                const int t = s.done_target;
+                hs[l].tgt_lane = lane_of[t] >= 0 ? lane_of[t] : -2;
+                hs[l].tgt_pos = (cfg->agents[t].init_row << 16) | cfg->agents[t].init_col;
+            }
+            if (s.destroy_target >= 0) hs[l].dtgt_lane = lane_of[s.destroy_target] >= 0 ? lane_of[s.destroy_target] : -2;
+        }
     }
     HIPCHK(hipMalloc(&g->d_spec, sizeof(DevAgent) * A));
     HIPCHK(hipMemcpy(g->d_spec, hs, sizeof(DevAgent) * A, hipMemcpyHostToDevice));

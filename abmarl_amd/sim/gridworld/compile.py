@@ -18,7 +18,7 @@ from abmarl_amd.sim.gridworld.agent import (
 from abmarl_amd.sim.gridworld.components import (
     PositionState, HealthState, OrientationState, BinaryAttackActor, SelectiveAttackActor,
     PositionCenteredEncodingObserver, AbsoluteEncodingObserver, ActiveDone, OneTeamRemainingDone,
-    MoveActor, DriftMoveActor)
+    TargetAgentDone, TargetDestroyedDone, MoveActor, DriftMoveActor)
 
 
 class UnsupportedConfig(ValueError):
@@ -148,6 +148,9 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
             raise UnsupportedConfig(f"{type(x).__name__} has no HIP implementation")
 
     done_kind = 0
+    ids = list(sim.agents)
+    done_target = [-1] * n
+    destroy_target = [-1] * n
     for d in dones:
         if getattr(d, '_program_done', None) == program:
             continue                          # decided by the sim program itself
@@ -155,13 +158,29 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
             done_kind |= _abi.GW_DONE_ONE_TEAM
         elif isinstance(d, ActiveDone):
             done_kind |= _abi.GW_DONE_ACTIVE
+        elif isinstance(d, (TargetAgentDone, TargetDestroyedDone)):
+            if sum(isinstance(x, type(d)) for x in dones) > 1:
+                raise UnsupportedConfig(f"one {type(d).__name__} per simulation")
+            tgt = done_target if isinstance(d, TargetAgentDone) else destroy_target
+            done_kind |= _abi.GW_DONE_TARGET_AGENT if isinstance(d, TargetAgentDone) \
+                else _abi.GW_DONE_TARGET_DESTROYED
+            for aid, tid in d.target_mapping.items():
+                tgt[ids.index(aid)] = ids.index(tid)
+            for i, a in enumerate(agents):
+                if tgt[i] < 0 and isinstance(a, ObservingAgent) and isinstance(a, ActingAgent):
+                    # get_done(agent) indexes target_mapping[agent.id] (done.py:91,131)
+                    raise UnsupportedConfig(f"{a.id} is not in {type(d).__name__}.target_mapping "
+                                            "(the reference raises KeyError in get_done)")
         else:
             raise UnsupportedConfig(f"{type(d).__name__} has no HIP implementation")
     # OneTeamRemainingDone.get_done is ActiveDone.get_done (done.py:140)
     order = {'position_health': _abi.GW_ORDER_POSITION_HEALTH,
              'health_position': _abi.GW_ORDER_HEALTH_POSITION}[state_order]
+    specs = [agent_spec(a, program_type, food_type) for a in agents]
+    for i, s in enumerate(specs):
+        s.done_target, s.destroy_target = done_target[i], destroy_target[i]
     return _abi.CompiledConfig(
-        sim.grid.rows, sim.grid.cols, [agent_spec(a, program_type, food_type) for a in agents],
+        sim.grid.rows, sim.grid.cols, specs,
         program,
         sim.grid.overlap_bits(), amap, stacked_attacks=stacked, observe_self=observe_self,
         no_overlap_at_reset=pos_states[0].no_overlap_at_reset, state_order=order,

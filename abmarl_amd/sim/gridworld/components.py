@@ -6,7 +6,7 @@ fused HIP step instead of here.  What each one contributes to the compiled
 engine configuration is in ``abmarl_amd/sim/gridworld/compile.py``.
 
 Reference: abmarl/sim/gridworld/state.py:13-166,622-641; actor.py:13-114,
-237-501; observer.py:13-52,153-250; done.py:10-56,140-153.
+237-501; observer.py:13-52,153-250; done.py:10-153.
 """
 from abc import ABC, abstractmethod
 
@@ -15,7 +15,7 @@ import numpy as np
 from abmarl_amd.spaces import Box, Discrete
 from abmarl_amd.sim.gridworld.base import GridWorldBaseComponent
 from abmarl_amd.sim.gridworld.agent import (
-    GridObservingAgent, MovingAgent, AttackingAgent, OrientationAgent)
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, OrientationAgent)
 
 
 class _EngineExecuted:
@@ -243,3 +243,38 @@ class ActiveDone(DoneBaseComponent):
 
 class OneTeamRemainingDone(ActiveDone):
     """done.py:140-153: all done when the active agents share <= 1 encoding."""
+
+
+class _TargetMappingDone(DoneBaseComponent):
+    """The target_mapping property shared by done.py:59-99 and :102-137."""
+
+    def __init__(self, target_mapping=None, **kwargs):
+        super().__init__(**kwargs)
+        self.target_mapping = target_mapping
+
+    @property
+    def target_mapping(self):
+        """Maps the agent to its respective target (by agent id)."""
+        return self._target_mapping
+
+    @target_mapping.setter
+    def target_mapping(self, value):
+        assert type(value) is dict, "Target mapping must be a dictionary."
+        for agent_id, target_id in value.items():
+            assert agent_id in self.agents, f"{agent_id} must be an agent in the simulation."
+            assert isinstance(self.agents[agent_id], GridWorldAgent), \
+                f"{agent_id} must be a GridWorldAgent."
+            assert target_id in self.agents, "Target must be an agent in the simulation."
+            assert isinstance(self.agents[target_id], GridWorldAgent), \
+                "Target must be a GridWorldAgent."
+        self._target_mapping = value
+
+
+class TargetAgentDone(_TargetMappingDone):
+    """done.py:59-99: an agent is done when it is on its target's position
+    (np.array_equal of the positions); all done when every mapped agent is."""
+
+
+class TargetDestroyedDone(_TargetMappingDone):
+    """done.py:102-137: an agent is done when its target is inactive; all
+    done when every mapped agent's target is."""

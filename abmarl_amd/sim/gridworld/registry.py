@@ -5,7 +5,8 @@ other subclass raises, because the fused step cannot run arbitrary Python.
 """
 from abmarl_amd.sim.gridworld.components import (
     ActorBaseComponent, MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor,
-    SelectiveAttackActor, DoneBaseComponent, ActiveDone, OneTeamRemainingDone,
+    SelectiveAttackActor, DoneBaseComponent, ActiveDone, OneTeamRemainingDone, TargetAgentDone,
+    TargetDestroyedDone,
     ObserverBaseComponent, PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
     StateBaseComponent, PositionState, HealthState, OrientationState,
 )
@@ -19,7 +20,7 @@ _subclass_check_mapping = {
 
 _registered_components = {
     'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor},
-    'done': {ActiveDone, OneTeamRemainingDone},
+    'done': {ActiveDone, OneTeamRemainingDone, TargetAgentDone, TargetDestroyedDone},
     'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
     'state': {PositionState, HealthState, OrientationState},
 }

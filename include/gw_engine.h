@@ -123,6 +123,9 @@ typedef int32_t gw_status;
 #define GW_SIM_REACH_TARGET 3   /* examples/sim/reach_the_target.py:84-158   */
 #define GW_SIM_PACMAN       4   /* examples/sim/pacman.py:29-158: DriftMoveActor moves, the
                                    tunnel, food and baddies (see "Pacman program" below) */
+#define GW_SIM_TRAFFIC      5   /* examples/sim/traffic_corridor.py:24-49: moves in dict order,
+                                   -0.1 on a failed move, +1 when get_done(agent) right after
+                                   its move (the done components, e.g. TargetAgentDone)     */
 
 /* observer of the sim's GridObservingAgents */
 #define GW_OBS_POSITION_CENTERED 0  /* observer.py:153-250: (2v+1)^2 window, -1 off-grid   */
@@ -136,6 +139,13 @@ typedef int32_t gw_status;
 /* done components (bit set; get_done = AND, get_all_done = AND: smart.py:106-117) */
 #define GW_DONE_ACTIVE        0x1u /* ActiveDone            done.py:39-56   */
 #define GW_DONE_ONE_TEAM      0x2u /* OneTeamRemainingDone  done.py:140-153 */
+#define GW_DONE_TARGET_AGENT  0x4u /* TargetAgentDone       done.py:59-99: done = on the
+                                      position of gw_agent_spec.done_target; all done = every
+                                      mapped entity done                                   */
+#define GW_DONE_TARGET_DESTROYED 0x8u /* TargetDestroyedDone done.py:102-137: done = the entity
+                                      gw_agent_spec.destroy_target is inactive; all done = every
+                                      mapped entity's target inactive                      */
+/* done_kind 0 (no done component) is the reference's all([]): every agent done. */
 
 /* reset-time state component order (SmartGridWorldSimulation iterates a set) */
 #define GW_ORDER_POSITION_HEALTH 0
@@ -153,6 +163,8 @@ typedef struct gw_agent_spec {
     double   attack_accuracy;
     double   initial_health;       /* < 0 means None (uniform(0,1) at reset)   */
     int32_t  initial_orientation;  /* OrientationAgent: 1..4, 0 = None (randint(1, 5)) */
+    int32_t  done_target;          /* TargetAgentDone.target_mapping[this] (entity index), -1 */
+    int32_t  destroy_target;       /* TargetDestroyedDone.target_mapping[this], -1            */
 } gw_agent_spec;
 
 typedef struct gw_config {

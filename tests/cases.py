@@ -11,7 +11,8 @@ from abmarl_amd.sim.gridworld.agent import (
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
-                'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double', 'rtt_64']
+                'tb_destroy', 'tb_chase', 'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double',
+                'rtt_64', 'traffic_ex', 'traffic_9']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -65,10 +66,36 @@ RTT_CONFIG4 = dict(kind='rtt', rows=64, cols=64, n_barriers=128, n_runners=127, 
                    target=dict(view_range=3, attack_range=1, attack_strength=1, attack_accuracy=1))
 
 
+def build_traffic(c):
+    """TrafficCorridor as in the reference's examples/rllib_traffic_corridor_2_teams.py."""
+    from abmarl_amd.examples.traffic_corridor import (
+        TrafficCorridorSimulation, TrafficAgent, TargetAgent, WallAgent)
+    reg = {
+        'R': lambda n: TrafficAgent(id=f'red{n}', encoding=1),
+        'G': lambda n: TrafficAgent(id=f'green{n}', encoding=2),
+        'r': lambda n: TargetAgent(id='red_target', encoding=1),
+        'g': lambda n: TargetAgent(id='green_target', encoding=2),
+        'W': lambda n: WallAgent(id=f'wall{n}', encoding=3),
+    }
+    arr = np.array([list(r) for r in c['grid']], dtype=object)
+    kw = dict(overlapping={1: {1}, 2: {2}}, states={'PositionState'},
+              observers={'PositionCenteredEncodingObserver'})
+    ids = list(TrafficCorridorSimulation.build_sim_from_array(arr, reg, **kw).agents)
+    if c.get('targets') == 'team':
+        mapping = {a: ('red_target' if a.startswith('red') else 'green_target')
+                   for a in ids if a.startswith(('red', 'green')) and not a.endswith('_target')}
+    else:
+        mapping = dict(c['target_mapping'])
+    return TrafficCorridorSimulation.build_sim_from_array(arr, reg, dones={'TargetAgentDone'},
+                                                          target_mapping=mapping, **kw)
+
+
 def build_sim(c):
     """The golden case's configuration, built with the host API."""
     if c.get('kind') == 'maze':
         return build_maze(c)
+    if c.get('kind') == 'traffic':
+        return build_traffic(c)
     if c.get('kind') == 'rtt':
         return build_rtt(c)
     agents = {}
@@ -88,7 +115,9 @@ def build_sim(c):
         no_overlap_at_reset=c['no_overlap_at_reset'],
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
-        dones={'OneTeamRemainingDone'}, state_order=c['state_order'])
+        dones=set(c.get('dones', ['OneTeamRemainingDone'])), state_order=c['state_order'])
+    if 'target_mapping' in c:
+        kwargs['target_mapping'] = dict(c['target_mapping'])
     if c.get('walls'):
         arr = np.full((c['rows'], c['cols']), '_', dtype=object)
         for r, cc in c['walls']:

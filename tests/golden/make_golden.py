@@ -89,6 +89,27 @@ CASES = [
          runner=dict(move_range=2, view_range=3, initial_health=1),
          target=dict(view_range=3, attack_range=1, attack_strength=1, attack_accuracy=1)),
     # MazeNavigation 16x16 from generate_maze (utils.py:120-212), N and T on passages
+    # TeamBattle with the target done components (done.py:59-137): each
+    # fighter hunts the next one of the other team (TargetDestroyedDone) or
+    # chases it (TargetAgentDone)
+    dict(name='tb_destroy', rows=7, cols=7, n_agents=10, n_teams=2, n_envs=5, n_steps=120,
+         horizon=60, seed_base=61, dones=['ActiveDone', 'TargetDestroyedDone'],
+         target_mapping={i: (i + 1) % 10 for i in range(10)},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.8,
+                    view_range=2)),
+    dict(name='tb_chase', rows=6, cols=6, n_agents=8, n_teams=2, n_envs=5, n_steps=120,
+         horizon=50, seed_base=71, dones=['TargetAgentDone'],
+         target_mapping={i: (i + 3) % 8 for i in range(8)}, overlap={1: [1, 2], 2: [2]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.3, attack_accuracy=1,
+                    view_range=2)),
+    # TrafficCorridor: the reference example itself (examples/rllib_traffic_corridor_2_teams.py)
+    dict(name='traffic_ex', kind='traffic', n_envs=6, n_steps=150, horizon=40, seed_base=91,
+         grid=['GWWWR', 'r___g', 'GWWWR'],
+         target_mapping={'red4': 'red_target', 'red11': 'red_target', 'green0': 'green_target',
+                         'green7': 'green_target'}),
+    # a longer two-lane corridor with more traffic
+    dict(name='traffic_9', kind='traffic', n_envs=4, n_steps=150, horizon=60, seed_base=93,
+         grid=['G_WWWWW_R', 'G_______R', 'r___W___g', 'G_______R', 'G_WWWWW_R'], targets='team'),
     dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
          horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
 ]
@@ -119,6 +140,11 @@ def maze_array(spec):
 
 def full_case(case):
     c = dict(case)
+    if c.get('kind') == 'traffic':
+        c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
+        c['action_seed'] = 1234 + c['seed_base']
+        c['agent'] = dict(move_range=1, view_range=3)
+        return c
     if c.get('kind') == 'rtt':
         c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
         c['action_seed'] = 1234 + c['seed_base']
@@ -144,6 +170,9 @@ def full_case(case):
     c.setdefault('initial_positions', {})
     c.setdefault('initial_health', {})
     c.setdefault('agent', DEFAULT_AGENT)
+    c.setdefault('dones', ['OneTeamRemainingDone'])
+    if 'target_mapping' in c:
+        c['target_mapping'] = {f'agent{k}': f'agent{v}' for k, v in c['target_mapping'].items()}
     if c.pop('corners', False):
         corners = [[1, 1], [1, 6], [6, 1], [6, 6]]
         c['initial_positions'] = {i: corners[i % 4] for i in range(c['n_agents'])}
@@ -211,9 +240,45 @@ def build_reference_rtt(c):
     return AllStepManager(sim)
 
 
+def traffic_registry(TrafficAgent, TargetAgent, WallAgent):
+    """rllib_traffic_corridor_2_teams.py's object registry."""
+    return {
+        'R': lambda n: TrafficAgent(id=f'red{n}', encoding=1),
+        'G': lambda n: TrafficAgent(id=f'green{n}', encoding=2),
+        'r': lambda n: TargetAgent(id='red_target', encoding=1),
+        'g': lambda n: TargetAgent(id='green_target', encoding=2),
+        'W': lambda n: WallAgent(id=f'wall{n}', encoding=3),
+    }
+
+
+def traffic_mapping(c, ids):
+    if c.get('targets') == 'team':
+        return {a: ('red_target' if a.startswith('red') and a != 'red_target' else 'green_target')
+                for a in ids if a.startswith(('red', 'green')) and not a.endswith('_target')}
+    return dict(c['target_mapping'])
+
+
+def build_reference_traffic(c):
+    from abmarl.examples.sim.traffic_corridor import WallAgent, TargetAgent, TrafficAgent, \
+        TrafficCorridorSimulation
+    from abmarl.managers import AllStepManager
+    arr = np.array([list(r) for r in c['grid']], dtype=object)
+    reg = traffic_registry(TrafficAgent, TargetAgent, WallAgent)
+    probe = TrafficCorridorSimulation.build_sim_from_array(
+        arr, reg, overlapping={1: {1}, 2: {2}}, states={'PositionState'},
+        observers={'PositionCenteredEncodingObserver'})
+    mapping = traffic_mapping(c, list(probe.agents))
+    sim = TrafficCorridorSimulation.build_sim_from_array(
+        arr, reg, overlapping={1: {1}, 2: {2}}, states={'PositionState'}, dones={'TargetAgentDone'},
+        observers={'PositionCenteredEncodingObserver'}, target_mapping=mapping)
+    return AllStepManager(sim)
+
+
 def build_reference_env(c):
     if c['kind'] == 'maze':
         return build_reference_maze(c)
+    if c['kind'] == 'traffic':
+        return build_reference_traffic(c)
     if c['kind'] == 'rtt':
         return build_reference_rtt(c)
     from abmarl.examples.sim.team_battle_example import TeamBattleSim
@@ -244,7 +309,9 @@ def build_reference_env(c):
         no_overlap_at_reset=c['no_overlap_at_reset'],
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
-        dones={'OneTeamRemainingDone'})
+        dones=set(c['dones']))
+    if 'target_mapping' in c:
+        kwargs['target_mapping'] = dict(c['target_mapping'])
     if c['walls']:
         arr = np.full((c['rows'], c['cols']), '_', dtype=object)
         for r, cc in c['walls']:
@@ -321,6 +388,8 @@ def run_case(case):
                             d = 2 * ag.attack_range + 1
                             a['attack'] = act[t, e, i, 2:2 + d * d].astype(int).reshape(d, d)
                         adict[aid] = a
+                    elif c['kind'] == 'traffic':
+                        adict[aid] = {'move': act[t, e, i, :2].astype(int)}
                     else:
                         adict[aid] = {'move': act[t, e, i, :2].astype(int),
                                       'attack': int(act[t, e, i, 2])}

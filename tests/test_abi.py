@@ -48,18 +48,35 @@ def test_constants_match_header():
             assert getattr(_abi, name) == val, name
 
 
-def test_struct_layout():
-    # gw_agent_spec: 8 int32 + 3 double + int32 (+4 padding) = 64 bytes
-    assert C.sizeof(_abi.AgentSpec) == 64
-    assert _abi.Config.agents.offset % 8 == 0
-    assert _abi.Config.pac_rewards.offset % 8 == 0
+def test_struct_layout(tmp_path):
+    """The ctypes mirror of gw_agent_spec / gw_config has the C compiler's
+    size and field offsets (a tiny C program compiled against the header)."""
+    import subprocess
+    fields = {'gw_agent_spec': [f for f, _ in _abi.AgentSpec._fields_],
+              'gw_config': [f for f, _ in _abi.Config._fields_]}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', 'int main(void) {']
+    for st, fs in fields.items():
+        lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fs:
+            lines.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    lines += ['return 0; }']
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(lines))
+    exe = tmp_path / 'layout'
+    subprocess.check_call(['gcc', '-o', str(exe), str(src)])
+    got = dict(line.rsplit(' ', 1) for line in subprocess.check_output([str(exe)]).decode().split('\n') if line)
+    py = {'gw_agent_spec': _abi.AgentSpec, 'gw_config': _abi.Config}
+    for st, cls in py.items():
+        assert int(got[st]) == C.sizeof(cls), st
+        for f in fields[st]:
+            assert int(got[f'{st}.{f}']) == getattr(cls, f).offset, f'{st}.{f}'
 
 
 def test_create_rejects_bad_config_without_gpu(lib):
     # argument validation happens before any HIP call
     h = C.c_void_p()
     assert lib.gw_create(None, 4, 0, C.byref(h)) == _abi.GW_E_INVALID
-    assert lib.gw_abi_version() == 3
+    assert lib.gw_abi_version() == 4
 
 
 def test_oracle_exports(oracle_mod):

@@ -92,6 +92,33 @@ def test_maze_navigation_1024_envs(oracle_mod):
 
 
 @pytest.mark.parametrize('kw', [
+    # TargetDestroyedDone (+ ActiveDone): hunt the next fighter of the other team
+    dict(rows=12, cols=12, n_agents=30, n_teams=2, dones=['ActiveDone', 'TargetDestroyedDone'],
+         target_mapping={f'agent{i}': f'agent{(i + 1) % 30}' for i in range(30)},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.8,
+                    view_range=3)),
+    # TargetAgentDone alone, cross-team overlap: chasers end on their target's cell
+    dict(rows=8, cols=8, n_agents=16, n_teams=2, dones=['TargetAgentDone'],
+         overlap={'1': [1, 2], '2': [2]},
+         target_mapping={f'agent{i}': f'agent{(i + 5) % 16}' for i in range(16)},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.3, attack_accuracy=1,
+                    view_range=2)),
+])
+def test_target_done_configs(oracle_mod, kw):
+    """TeamBattle with the target done components (done.py:59-137) at 1024 envs."""
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=1024, T=150, horizon=60, seed_run=8, key=13)
+
+
+@pytest.mark.parametrize('case', ['traffic_ex', 'traffic_9'])
+def test_traffic_corridor_configs(oracle_mod, case):
+    """TrafficCorridor (traffic_corridor.py, TargetAgentDone) at 1024 envs."""
+    from tests.cases import build_traffic
+    cc = build_traffic(load_golden(case)['case']).compiled()
+    _run(oracle_mod, cc, E=1024, T=200, horizon=60, seed_run=9, key=17)
+
+
+@pytest.mark.parametrize('kw', [
     # static blocking walls + blocking fighters, attack range 2 (attack mask)
     dict(rows=16, cols=16, n_agents=40, n_teams=2, wall_encoding=3, blocking=list(range(0, 40, 3)),
          walls=[[r, 7] for r in range(2, 12)] + [[4, c] for c in range(9, 15)] + [[12, 2], [13, 13]],

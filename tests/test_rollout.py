@@ -126,3 +126,10 @@ def test_rollout_workgroup_kernel():
     a, b = _pair(cc, 64, run=7, stagger=20)
     assert a.wg
     _compare(a, b, 0, horizon=20, mode='next_step', frags=(12, 12), allow_err=True)
+
+
+def test_rollout_traffic_corridor():
+    from tests.cases import build_traffic
+    cc = build_traffic(load_golden('traffic_9')['case']).compiled()
+    a, b = _pair(cc, 256, run=8, stagger=30)
+    _compare(a, b, 0, horizon=30, mode='next_step', frags=(40, 40))
