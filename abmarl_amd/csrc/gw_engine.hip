@@ -140,6 +140,13 @@ struct Params {
     int32_t nsteps;
     const uint8_t* ad_in;
     int32_t skip_done_obs;
+    // observers with different view ranges: slot-geometry (S x S) shadow LUT
+    // and static-blocker masks per range (bit wr * S + wc), offsets per range
+    int32_t hetero_view;
+    const uint32_t* hshadow;
+    const uint32_t* hsmask;
+    int32_t hshadow_off[GW_MAX_RANGE + 1];
+    int32_t hsmask_off[GW_MAX_RANGE + 1];
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -730,6 +737,11 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me)
                         : (p.skip_done_obs ? __ballot(l < A && !obs_me) : 0ull);
     if (l < A) L.obs_m2 = p.persistent_obs && !obs_me;
+    // observers with different view ranges (p.hetero_view): lane l's window
+    // of range vw <= R sits in the top-left (2vw+1)^2 of its S x S slot, the
+    // rest of the slot is -2 (the reference's per-agent (2v+1)^2 obs,
+    // observer.py:162-174, in one tensor shape)
+    const int vw = p.hetero_view ? (obs_me ? L.view : 0) : R;
 
     // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
     // static blockers precomputed per cell, blocking lanes from the shadow LUT
@@ -737,7 +749,26 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     uint32_t hid[MW];
 #pragma unroll
     for (int w = 0; w < MW; w++) hid[w] = 0u;
-    if (p.blockers) {
+    if (p.blockers && p.hetero_view) {
+        // slot-geometry LUTs per range (bit wr * S + wc)
+        if (obs_me && p.hsmask_off[vw] >= 0) {
+            const uint32_t* src = p.hsmask + p.hsmask_off[vw] + (size_t)(L.r * p.W + L.c) * MW;
+#pragma unroll
+            for (int w = 0; w < MW; w++) hid[w] = src[w];
+        }
+        if (p.lane_blockers) {
+            for (uint64_t bl = __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
+                const int b = first_lane(bl);
+                const int dr = rl(L.r, b) - L.r, dc = rl(L.c, b) - L.c;
+                if (obs_me && dr >= -vw && dr <= vw && dc >= -vw && dc <= vw && (dr != 0 || dc != 0)) {
+                    const uint32_t* src = p.hshadow + p.hshadow_off[vw] +
+                                          ((dr + vw) * (2 * vw + 1) + (dc + vw)) * MW;
+#pragma unroll
+                    for (int w = 0; w < MW; w++) hid[w] |= src[w];
+                }
+            }
+        }
+    } else if (p.blockers) {
         if (obs_me && p.smask_off[R] >= 0) {
             const uint32_t* src = p.smask + p.smask_off[R] + (size_t)(L.r * p.W + L.c) * MW;
 #pragma unroll
@@ -761,15 +792,18 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     // observation values (0 empty, enc, 0xFF = -1 off-grid); 0x80 marks a
     // crowded cell, resolved below; hidden cells become 0xFE = -2.
     uint32_t nev = 0;                         // crowded visible cells of this observer
-    auto stage_rows = [&](auto masked) {
+    auto stage_rows = [&](auto masked, auto hetero) {
         constexpr bool MASKED = decltype(masked)::value;
+        constexpr bool HETERO = decltype(hetero)::value;
         uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
         const uint32_t* t32 = (const uint32_t*)sm.tbl;
         uint32_t rows[S][ND];
-        const int o0 = tbl_idx(p, L.r - R, L.c - R);
+        const int o0 = HETERO ? tbl_idx(p, L.r - vw, L.c - vw) : tbl_idx(p, L.r - R, L.c - R);
+        const int D = 2 * vw + 1;                   // HETERO: this lane's window side
 #pragma unroll
         for (int wr = 0; wr < S; wr++) {
-            const int o = o0 + wr * p.pitch;
+            // HETERO: rows past the window re-read its last row (in the table), then masked
+            const int o = o0 + (HETERO ? min(wr, D - 1) : wr) * p.pitch;
 #pragma unroll
             for (int d = 0; d < ND; d++)
                 rows[wr][d] = t32[CIDX((o >> 2) + d, (p.tbl_rows * p.pitch + 3) / 4, 2)];
@@ -781,7 +815,16 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
 #pragma unroll
             for (int d = 0; d < NW; d++) {
                 uint32_t w = __builtin_amdgcn_alignbyte(rows[wr][d + 1], rows[wr][d], sh);
-                if (wr == R && d == R / 4 && self_fix) {        // alone on my cell, not observing myself
+                if constexpr (HETERO) {
+                    if (wr == vw && d == (vw >> 2) && self_fix) {   // my cell at (vw, vw)
+                        const int bs = 8 * (vw & 3);
+                        if (((w >> bs) & 0xffu) != CELL_CROWD) w &= ~(0xffu << bs);
+                    }
+                    // slot cells outside the window: -2
+                    const int nb = wr < D ? (D - 4 * d) : 0;
+                    const uint32_t keep = nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+                    w = (w & keep) | (0xFEFEFEFEu & ~keep);
+                } else if (wr == R && d == R / 4 && self_fix) {  // alone on my cell, not observing myself
                     constexpr int bs = 8 * (R & 3);
                     if (((w >> bs) & 0xffu) != CELL_CROWD) w &= ~(0xffu << bs);
                 }
@@ -803,8 +846,16 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     };
     if (l < A) {
         if (obs_me) {
-            if (p.blockers) stage_rows(std::integral_constant<bool, true>());
-            else stage_rows(std::integral_constant<bool, false>());
+            using T = std::integral_constant<bool, true>;
+            using F = std::integral_constant<bool, false>;
+            if (p.hetero_view) {
+                if (p.blockers) stage_rows(T(), T());
+                else stage_rows(F(), T());
+            } else if (p.blockers) {
+                stage_rows(T(), F());
+            } else {
+                stage_rows(F(), F());
+            }
         } else {
             uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
             // -2 rows; a row the store skips holds the 0x80 sentinel instead
@@ -871,7 +922,8 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             const int orr = __shfl(L.r, o), occ = __shfl(L.c, o);
             const uint32_t oseq = __shfl(L.seq, o);
             const bool o_in = __shfl((int)L.in_grid, o) != 0;
-            const int gr = orr - R + pwr, gc = occ - R + pwc;
+            const int ov = p.hetero_view ? __shfl(vw, o) : R;     // the observer's window origin
+            const int gr = orr - ov + pwr, gc = occ - ov + pwc;
             const int gcell = gr * p.W + gc;
             const bool self_in = !p.observe_self && o_in && orr == gr && occ == gc;
             uint32_t n = act ? cnt_get(sm.cnt, gcell) : 1u;
@@ -929,6 +981,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         const int o = first_lane(olanes);
         olanes &= olanes - 1;
         const int orr = rl(L.r, o), oc = rl(L.c, o);
+        const int ov = p.hetero_view ? rl(vw, o) : R;
         for (int k0 = 0; k0 < SS; k0 += WAVE) {
             const int k = k0 + l;
             const int sidx = o * SSP + (k / S) * SP + k % S;
@@ -937,7 +990,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             while (bits) {
                 const int kk = k0 + (int)__builtin_ctzll(bits);
                 bits &= bits - 1;
-                const int gr = orr - R + kk / S, gc = oc - R + kk % S;
+                const int gr = orr - ov + kk / S, gc = oc - ov + kk % S;
                 const bool mem = l < A && L.in_grid && L.r == gr && L.c == gc && (p.observe_self || l != o);
                 const uint64_t mm = __ballot(mem);
                 const int n = __popcll(mm);
@@ -2429,6 +2482,8 @@ struct gw_engine {
     uint32_t* d_static_bits;
     uint32_t* d_shadow;
     uint32_t* d_smask;
+    uint32_t* d_hshadow;       // slot-geometry LUTs (observers with different ranges)
+    uint32_t* d_hsmask;
     int32_t lane_ent[GW_MAX_LANES];
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     PolicySpec policy;
@@ -2568,8 +2623,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
         if (s.encoding < 1 || s.encoding > GW_MAX_ENC) { set_err("agent %d encoding %d", a, s.encoding); return GW_E_UNSUPPORTED; }
-        if ((s.kind & GW_K_GRID_OBSERVER) && cfg->obs_kind != GW_OBS_ABSOLUTE && s.view_range != cfg->obs_range) {
-            set_err("agent %d view_range %d != obs_range %d", a, s.view_range, cfg->obs_range);
+        if ((s.kind & GW_K_GRID_OBSERVER) && cfg->obs_kind != GW_OBS_ABSOLUTE &&
+            (s.view_range < 0 || s.view_range > cfg->obs_range)) {
+            set_err("agent %d view_range %d outside 0..obs_range %d", a, s.view_range, cfg->obs_range);
             return GW_E_UNSUPPORTED;
         }
         if ((s.kind & GW_K_ATTACKING) && (s.attack_range < 0 || s.attack_range > GW_MAX_RANGE)) {
@@ -2864,6 +2920,62 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             p.smask = g->d_smask;
         }
     }
+    // observers with different view ranges: their windows sit top-left in an
+    // S x S slot; the blocking LUTs are re-laid out in slot geometry per range
+    for (int l = 0; l < A; l++)
+        if ((hs[l].kind & GW_K_GRID_OBSERVER) && !pac && hs[l].view_range != cfg->obs_range) p.hetero_view = 1;
+    for (int r = 0; r <= GW_MAX_RANGE; r++) { p.hshadow_off[r] = -1; p.hsmask_off[r] = -1; }
+    if (p.hetero_view && wg) {
+        set_err("observers with different view ranges run on the one-wave kernel only");
+        return GW_E_UNSUPPORTED;
+    }
+    if (p.hetero_view && any_block) {
+        const int S = g->S, MWS = mask_words(cfg->obs_range), R = cfg->obs_range;
+        bool used[GW_MAX_RANGE + 1] = {};
+        for (int l = 0; l < A; l++) if (hs[l].kind & GW_K_GRID_OBSERVER) used[hs[l].view_range] = true;
+        // slot bits of the cells a blocker at (dr, dc) hides from a range-v window
+        auto slot_shadow = [&](int v, int dr, int dc, uint32_t* out) {
+            uint32_t b[16];
+            host_shadow(v, dr, dc, b);
+            const int D = 2 * v + 1;
+            for (int k = 0; k < D * D; k++)
+                if ((b[k >> 5] >> (k & 31)) & 1u) {
+                    const int q = (k / D) * S + (k % D);
+                    out[q >> 5] |= 1u << (q & 31);
+                }
+        };
+        std::vector<uint32_t> hl, hm;
+        std::vector<int> sblock;
+        for (int a : statics) if (cfg->agents[a].kind & GW_K_BLOCKING) sblock.push_back(a);
+        for (int v = 0; v <= R; v++) {
+            if (!used[v]) continue;
+            const int D = 2 * v + 1;
+            p.hshadow_off[v] = (int)hl.size();
+            hl.resize(hl.size() + (size_t)D * D * MWS, 0u);
+            for (int dr = -v; dr <= v; dr++)
+                for (int dc = -v; dc <= v; dc++)
+                    slot_shadow(v, dr, dc, hl.data() + p.hshadow_off[v] + ((dr + v) * D + (dc + v)) * MWS);
+            if (sblock.empty()) continue;
+            p.hsmask_off[v] = (int)hm.size();
+            hm.resize(hm.size() + (size_t)HW * MWS, 0u);
+            for (int cell = 0; cell < HW; cell++) {
+                const int cr = cell / cfg->cols, cc = cell % cfg->cols;
+                for (int a : sblock) {
+                    const int dr = cfg->agents[a].init_row - cr, dc = cfg->agents[a].init_col - cc;
+                    if (dr < -v || dr > v || dc < -v || dc > v || (dr == 0 && dc == 0)) continue;
+                    slot_shadow(v, dr, dc, hm.data() + p.hsmask_off[v] + (size_t)cell * MWS);
+                }
+            }
+        }
+        HIPCHK(hipMalloc(&g->d_hshadow, hl.size() * 4));
+        HIPCHK(hipMemcpy(g->d_hshadow, hl.data(), hl.size() * 4, hipMemcpyHostToDevice));
+        p.hshadow = g->d_hshadow;
+        if (!hm.empty()) {
+            HIPCHK(hipMalloc(&g->d_hsmask, hm.size() * 4));
+            HIPCHK(hipMemcpy(g->d_hsmask, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
+            p.hsmask = g->d_hsmask;
+        }
+    }
     p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
     g->smem_step = smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
@@ -2954,6 +3066,7 @@ gw_status gw_destroy(gw_handle g)
     (void)hipFree(g->d_static_bits); (void)hipFree(g->d_shadow); (void)hipFree(g->d_smask);
     (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
     (void)hipFree(g->d_passive); (void)hipFree(g->d_passive_enc);
+    (void)hipFree(g->d_hshadow); (void)hipFree(g->d_hsmask);
     delete g;
     return GW_OK;
 }

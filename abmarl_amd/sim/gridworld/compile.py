@@ -115,9 +115,8 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
         obs_kind = _abi.GW_OBS_ABSOLUTE
     elif pco:
         observe_self = pco[0].observe_self
-        if len(ranges) > 1:
-            raise UnsupportedConfig("all GridObservingAgents must share one view_range")
-        obs_range = ranges.pop() if ranges else 0
+        # different view ranges: each window top-left in a (2 max + 1)^2 slot
+        obs_range = max(ranges) if ranges else 0
     if obs_range > _abi.GW_MAX_RANGE:
         raise UnsupportedConfig(f"view_range > {_abi.GW_MAX_RANGE}")
 

@@ -11,8 +11,8 @@ from abmarl_amd.sim.gridworld.agent import (
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
-                'tb_destroy', 'tb_chase', 'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double',
-                'rtt_64', 'traffic_ex', 'traffic_9']
+                'tb_destroy', 'tb_chase', 'tb_views', 'maze_file', 'maze_16', 'rtt_7', 'rtt_7_views',
+                'rtt_16', 'rtt_double', 'rtt_64', 'traffic_ex', 'traffic_9']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -101,6 +101,8 @@ def build_sim(c):
     agents = {}
     for i in range(c['n_agents']):
         kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])
+        if c.get('views'):
+            kw['view_range'] = c['views'][i % len(c['views'])]
         if str(i) in c['initial_positions']:
             kw['initial_position'] = np.array(c['initial_positions'][str(i)])
         if str(i) in c['initial_health']:

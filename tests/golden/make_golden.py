@@ -110,6 +110,18 @@ CASES = [
     # a longer two-lane corridor with more traffic
     dict(name='traffic_9', kind='traffic', n_envs=4, n_steps=150, horizon=60, seed_base=93,
          grid=['G_WWWWW_R', 'G_______R', 'r___W___g', 'G_______R', 'G_WWWWW_R'], targets='team'),
+    # the reference's own ReachTheTarget example (examples/rllib_reach_the_target.py):
+    # runners see 3 cells, the target 7 (different view ranges)
+    dict(name='rtt_7_views', kind='rtt', rows=7, cols=7, n_barriers=10, n_runners=4, n_envs=4,
+         n_steps=120, horizon=40, seed_base=27, corners=True,
+         runner=dict(move_range=2, view_range=3, initial_health=1),
+         target=dict(view_range=7, attack_range=1, attack_strength=1, attack_accuracy=1)),
+    # TeamBattle with view ranges 1, 2 and 3 mixed, blocking walls and fighters
+    dict(name='tb_views', rows=10, cols=10, n_agents=18, n_teams=2, n_envs=4, n_steps=120,
+         horizon=60, seed_base=81, views=[1, 3, 2], walls=[[2, c] for c in range(2, 7)] +
+         [[r, 7] for r in range(4, 9)], wall_encoding=3, blocking=[0, 4, 9, 13],
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=3)),
     dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
          horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
 ]
@@ -148,7 +160,7 @@ def full_case(case):
     if c.get('kind') == 'rtt':
         c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
         c['action_seed'] = 1234 + c['seed_base']
-        c['agent'] = dict(view_range=c['runner']['view_range'])
+        c['agent'] = dict(view_range=max(c['runner']['view_range'], c['target']['view_range']))
         return c
     if c.get('kind') == 'maze':
         c['maze'] = maze_array(c['maze'])
@@ -294,6 +306,8 @@ def build_reference_env(c):
     agents = {}
     for i in range(c['n_agents']):
         kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])
+        if c.get('views'):
+            kw['view_range'] = c['views'][i % len(c['views'])]
         if str(i) in c['initial_positions']:
             kw['initial_position'] = np.array(c['initial_positions'][str(i)])
         if str(i) in c['initial_health']:
@@ -344,7 +358,9 @@ def run_case(case):
         ret = np.zeros(A, dtype=np.uint8)
         for i, aid in enumerate(ids):
             if aid in obs_dict:
-                out[i] = obs_dict[aid]['position_centered_encoding']
+                o = obs_dict[aid].get('position_centered_encoding')
+                if o is not None:           # a window of range v in the top-left of S x S
+                    out[i, :o.shape[0], :o.shape[1]] = o
                 ret[i] = 1
         return out, ret
 

@@ -103,7 +103,8 @@ def test_engine_autoreset_matches_reference(name):
     assert not eng.err.any().item()
 
 
-RTT_GOLDEN = [n for n in GOLDEN_CASES if n.startswith('rtt')]
+# the workgroup kernel has one view range (rtt_7_views: mixed, the one-wave kernel)
+RTT_GOLDEN = [n for n in GOLDEN_CASES if n.startswith('rtt') and n != 'rtt_7_views']
 
 
 @pytest.mark.parametrize('name', RTT_GOLDEN)

@@ -119,6 +119,22 @@ def test_traffic_corridor_configs(oracle_mod, case):
 
 
 @pytest.mark.parametrize('kw', [
+    # view ranges 1..4 mixed, blocking fighters and static walls (slot-geometry LUTs)
+    dict(rows=16, cols=16, n_agents=40, n_teams=2, wall_encoding=3, blocking=list(range(0, 40, 4)),
+         walls=[[r, 7] for r in range(2, 12)] + [[4, c] for c in range(9, 15)], views=[1, 4, 2, 3],
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.5, attack_accuracy=0.8,
+                    view_range=3)),
+    # observe_self=False, cross-team overlap (crowded cells with the observer's own cell)
+    dict(rows=10, cols=10, n_agents=36, n_teams=3, views=[2, 1, 3], observe_self=False,
+         overlap={'1': [1, 2], '2': [2], '3': [3, 1]}),
+])
+def test_mixed_view_configs(oracle_mod, kw):
+    """Observers with different view ranges (observer.py:162-174) at 1024 envs."""
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=1024, T=120, horizon=50, seed_run=12, key=21)
+
+
+@pytest.mark.parametrize('kw', [
     # static blocking walls + blocking fighters, attack range 2 (attack mask)
     dict(rows=16, cols=16, n_agents=40, n_teams=2, wall_encoding=3, blocking=list(range(0, 40, 3)),
          walls=[[r, 7] for r in range(2, 12)] + [[4, c] for c in range(9, 15)] + [[12, 2], [13, 13]],
