@@ -25,6 +25,13 @@ GW_ERR_NO_CELL = 1
 GW_ERR_INIT_POSITION = 2
 GW_ERR_DOUBLE_REMOVE = 4
 GW_ERR_TUNNEL_PLACE = 8
+GW_ERR_NOT_IN_GRID = 16
+
+GW_OP_POSITION_RESET = 1
+GW_OP_HEALTH_RESET = 2
+GW_OP_MOVE = 3
+GW_OP_ATTACK = 4
+GW_OP_OBSERVE = 5
 
 GW_K_OBSERVING = 0x01
 GW_K_ACTING = 0x02
@@ -115,6 +122,7 @@ class Config(C.Structure):
         ("pac_rewards", C.c_double * 5),
         ("force_workgroup", C.c_int32),
         ("persistent_obs", C.c_int32),
+        ("all_lanes", C.c_int32),
     ]
 
 

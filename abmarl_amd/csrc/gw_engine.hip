@@ -142,6 +142,10 @@ struct Params {
     int32_t skip_done_obs;
     // observers with different view ranges: slot-geometry (S x S) shadow LUT
     // and static-blocker masks per range (bit wr * S + wc), offsets per range
+    // gw_component: the op's result rows [E][2 + A] and the observed lane
+    // of OBSERVE (-1 otherwise: every live observer)
+    int32_t* comp_out;
+    int32_t obs_only;
     int32_t hetero_view;
     const uint32_t* hshadow;
     const uint32_t* hsmask;
@@ -729,7 +733,9 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     constexpr int SSP = S * SP;
     const int l = lane_id();
     const int A = p.A;
-    const bool obs_me = l < A && L.live && (L.kind & GW_K_GRID_OBSERVER);
+    // (gw_component OBSERVE: the one lane p.obs_only, whatever its done state)
+    const bool obs_me = (p.obs_only >= 0 ? l == p.obs_only : (l < A && L.live)) &&
+                        (L.kind & GW_K_GRID_OBSERVER);
     // persistent obs buffer (gw_config.persistent_obs): rows that already
     // hold -2 and stay -2 (done entities, non-observers) are not rewritten
     // (gw_rollout with skip_done_obs: rows of lanes without an observation
@@ -1459,7 +1465,10 @@ __device__ __forceinline__ bool targets_all_done(const Params& p, const Lane& L)
 // AllStepManager.reset (all_step_manager.py:37-49) -> SmartGWS.reset ->
 // PositionState.reset (state.py:88-166) / HealthState.reset (:629-641) in the
 // pinned order.  Returns false on the reference's placement exceptions.
-__device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr, uint32_t& err)
+// what: 1 PositionState only, 2 HealthState only (the component-level
+// gw_component ops), 3 both in the pinned state order (SmartGWS.reset)
+__device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr, uint32_t& err,
+                                         int what = 3)
 {
     const int l = lane_id();
     const int A = p.A;
@@ -1469,10 +1478,14 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     const int NF = p.n_free;
     auto to_cell = [&](int f) -> int { return p.free_cell ? (int)p.free_cell[CIDX(f, NF, 19)] : f; };
     auto to_free = [&](int cell) -> int { return p.cell_free ? (int)p.cell_free[CIDX(cell, p.H * p.W, 19)] : cell; };
-    L.live = valid && (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
-    L.in_grid = false;
-    L.reward = 0.0;
-    ctr = 0;
+    if (what == 3) {
+        L.live = valid && (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
+        L.reward = 0.0;
+    }
+    if (what & 1) {                         // Grid.reset (state.py:97): every cell empty
+        L.in_grid = false;
+        ctr = 0;
+    }
     rng.ensure_key();                       // placement / health read the key directly
     const bool has_health = __ballot(valid && (L.kind & GW_K_HEALTH)) != 0;
 
@@ -1864,8 +1877,12 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
 #ifdef GW_STAMPS
     const int e = blockIdx.x;
 #endif
-    bool ok;
-    if (p.state_order == GW_ORDER_POSITION_HEALTH) {
+    bool ok = true;
+    if (what == 1) {
+        ok = place();
+    } else if (what == 2) {
+        if (has_health) health_reset();
+    } else if (p.state_order == GW_ORDER_POSITION_HEALTH) {
         ok = place();
         STAMP(11);
         if (ok && has_health) health_reset();
@@ -1876,7 +1893,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         ok = place();
         STAMP(15);
     }
-    if (valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
+    if (what == 3 && valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
     return ok;
 }
 
@@ -2298,6 +2315,90 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     STAMP(6);
 }
 
+// The component plugin API (state.py / actor.py / observer.py), one
+// component call for ONE entity (lane p.obs_only) in every env: the wave
+// loads the env, runs the component's body as the fused programs do, and
+// stores the env back.  result[e] = {status, n, attacked lanes...}.
+template <int S>
+__global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int e = blockIdx.x;
+    if (e >= p.E) return;
+    const int l = lane_id();
+    const int A = p.A;
+    const bool valid = l < A;
+    Smem sm = carve(smem_raw, p);
+    Lane L;
+    load_lane(p, e, L, valid);
+    Rng rng;
+    uint32_t ctr;
+    load_env(p, e, sm, rng, ctr, true);
+    const int op = p.mode, a = p.obs_lane;
+    int32_t* res = p.comp_out ? p.comp_out + (size_t)e * (2 + A) : nullptr;
+    int status = 0, nlist = 0, list = -1;
+    uint32_t err = 0;
+    // the component's own parameters come with the call (gw_engine.h)
+    const int32_t* arg = p.actions ? p.actions + (size_t)e * p.act_dim : nullptr;
+    Params q = p;
+    if (op == GW_OP_POSITION_RESET || op == GW_OP_HEALTH_RESET) {
+        if (arg) q.no_overlap_at_reset = uni(arg[0]);
+        uint32_t c2 = ctr;
+        const bool ok = do_reset(q, sm, rng, L, c2, err, op == GW_OP_POSITION_RESET ? 1 : 2);
+        ctr = c2;
+        status = ok ? 1 : 0;
+    } else {
+        if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
+        build_tables(p, sm, L, false);
+        if (op == GW_OP_MOVE) {
+            // MoveActor.process_action (actor.py:82-114); None for non-MovingAgents
+            if (!(rl(L.kind, a) & GW_K_MOVING)) {
+                status = -1;
+            } else {
+                const int mr = uni(arg[0]), mc = uni(arg[1]);
+                const int ar = rl(L.r, a), ac = rl(L.c, a);
+                const bool in = rlb(L.in_grid, a);
+                const bool ok = move_one(p, L, a, mr, mc, ctr + (uint32_t)a);
+                // a move off a cell the agent is not in: Grid.remove raises KeyError
+                if (ok && !in && (rl(L.r, a) != ar || rl(L.c, a) != ac)) {
+                    err |= GW_ERR_NOT_IN_GRID;
+                    if (l == a) { L.r = ar; L.c = ac; }
+                }
+                if (ok && l == a && (L.r != ar || L.c != ac)) L.in_grid = true;
+                status = ok ? 1 : 0;
+                ctr += (uint32_t)WAVE;
+            }
+        } else if (op == GW_OP_ATTACK) {
+            // AttackActorBaseComponent.process_action (actor.py:306-361)
+            if (rl(L.kind, a) & GW_K_ATTACKING) {
+                const int f = uni(arg[0]);
+                q.stacked = f & 1;
+                const uint32_t amap = (uint32_t)uni(arg[1]);
+                const uint32_t keep = L.amap;
+                if (l == a) L.amap = amap;                  // attack_mapping[attacker's encoding]
+                const bool st = (f & 2)
+                    ? attack_selective(q, sm, rng, L, a, arg + 2, nlist, list)
+                    : attack_one(q, sm, rng, L, a, uni(arg[2]), nlist, list);
+                if (l == a) L.amap = keep;
+                status = st ? 1 : 0;
+            }
+        } else if (op == GW_OP_OBSERVE) {
+            if (arg) q.observe_self = uni(arg[0]);
+            q.obs_only = a;
+            q.skip_done_obs = 1;
+            q.persistent_obs = 0;
+            observe_all<S>(q, e, sm, rng, L, p.obs);
+        }
+    }
+    if (res) {
+        if (l == 0) { res[0] = status; res[1] = nlist; }
+        if (l < nlist && l < A) res[2 + l] = list;
+    }
+    if (l == 0 && p.err && err) p.err[e] |= err;
+    store_lane(p, e, L, valid);
+    store_rng(p, e, sm, rng, ctr);
+}
+
 template <int S>
 __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
 {
@@ -2431,7 +2532,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 // in their own translation unit (-DGW_PART_S=<S>; _native.build compiles the
 // parts in parallel and links them with the host part).  Each part exports a
 // launcher and an attribute setter; the host part dispatches on S to them.
-enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3 };
+enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4 };
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
@@ -2455,6 +2556,7 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     case PK_RESET: hipLaunchKernelGGL(reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_STEP: hipLaunchKernelGGL(wg_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_COMP: hipLaunchKernelGGL(comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2466,6 +2568,7 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
     const void* k = kind == PK_STEP ? (const void*)step_kernel<S>
                   : kind == PK_RESET ? (const void*)reset_kernel<S>
                   : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
+                  : kind == PK_COMP ? (const void*)comp_kernel<S>
                                        : (const void*)wg_reset_kernel<S>;
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
@@ -2692,7 +2795,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
         if (pac && (s.kind & GW_K_FOOD)) { passive.push_back(a); continue; }
-        const bool st = !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
+        const bool st = !cfg->all_lanes && !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
                         cfg->overlap[s.encoding] == 0 && !((overlapped >> s.encoding) & 1u) &&
                         !((attacked >> s.encoding) & 1u) &&
                         !((maze || rtt) && (a == cfg->nav_agent || a == cfg->target_agent));
@@ -2819,6 +2922,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.act_dim = gw_config_act_dim(cfg);
     p.attack_kind = cfg->attack_kind;
     p.persistent_obs = cfg->persistent_obs != 0;
+    p.obs_only = -1;
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
@@ -3052,7 +3156,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
     HIPCHK(hipMemset(p.racc, 0, EA * sizeof(double)));
     if (wg) HIPCHK(set_part_attrs(g->S, PK_WG_STEP, PK_WG_RESET, g->smem_step, g->smem_step));
-    else HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
+    else if (!pac) HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
+    if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
     *out = g;
     return GW_OK;
 }
@@ -3325,6 +3430,26 @@ gw_status gw_rollout_step(gw_handle g, uint64_t key, uint32_t step, uint32_t env
     p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
     p.nsteps = 1; p.ad_in = all_done;
     HIPCHK(do_step(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
+                       int32_t* obs, uint32_t* err_flags, void* stream)
+{
+    if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_OBSERVE) return GW_E_INVALID;
+    if (g->wg || g->pacman) {
+        set_err("component operations run on the one-wave engine (not the workgroup / Pacman kernels)");
+        return GW_E_UNSUPPORTED;
+    }
+    const bool needs_lane = op == GW_OP_MOVE || op == GW_OP_ATTACK || op == GW_OP_OBSERVE;
+    if (needs_lane && (lane < 0 || lane >= g->A)) { set_err("lane %d outside 0..%d", lane, g->A - 1); return GW_E_INVALID; }
+    if ((op == GW_OP_MOVE || op == GW_OP_ATTACK) && !args) return GW_E_INVALID;
+    if (op == GW_OP_ATTACK && g->base.act_dim < 3) return GW_E_INVALID;
+    if (op == GW_OP_OBSERVE && !obs) return GW_E_INVALID;
+    Params p = g->base;
+    p.mode = op; p.obs_lane = lane; p.actions = args; p.comp_out = result; p.obs = obs; p.err = err_flags;
+    p.nsteps = 1;
+    HIPCHK(part_launch(g, PK_COMP, g->smem_step, p, (hipStream_t)stream));
     return GW_OK;
 }
 

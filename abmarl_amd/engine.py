@@ -242,6 +242,42 @@ class GridWorldEngine:
 
     AUTORESET_MODES = {'none': 0, 'same_step': 1, 'next_step': 2}
 
+    # ------------------------------------------------ component plugin API
+    def component(self, op, lane=-1, args=None, result=None, obs=None):
+        """One component operation (gw_component, GW_OP_*) for entity `lane`
+        in every env: args int32[E][act_dim] (MOVE / ATTACK), result
+        int32[E][2 + A] (status, n attacked, attacked lanes), obs (OBSERVE)."""
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_component(self.h, int(op), int(lane), _ptr(args), _ptr(result),
+                                              _ptr(obs), _ptr(self.err), _stream()), 'gw_component')
+        return result
+
+    def move(self, lane, moves):
+        """MoveActor.process_action for entity `lane` in every env (batched):
+        moves int32[E][2]; returns status int32[E] (1 True, 0 False, -1 None)."""
+        args = torch.zeros((self.E, self.act_dim), dtype=torch.int32, device=self.device)
+        args[:, :2] = moves
+        res = torch.zeros((self.E, 2 + self.A), dtype=torch.int32, device=self.device)
+        self.component(_abi.GW_OP_MOVE, lane, args, res)
+        return res[:, 0]
+
+    def attack(self, lane, attack):
+        """The attack actor's process_action for entity `lane` in every env:
+        attack int32[E] (binary) or int32[E][(2r+1)^2] (selective); returns
+        (status int32[E], n int32[E], attacked lanes int32[E][A])."""
+        args = torch.zeros((self.E, self.act_dim), dtype=torch.int32, device=self.device)
+        a = torch.as_tensor(attack, dtype=torch.int32, device=self.device).reshape(self.E, -1)
+        args[:, 2:2 + a.shape[1]] = a
+        res = torch.zeros((self.E, 2 + self.A), dtype=torch.int32, device=self.device)
+        self.component(_abi.GW_OP_ATTACK, lane, args, res)
+        return res[:, 0], res[:, 1], res[:, 2:]
+
+    def observe_lane(self, lane):
+        """PositionCenteredEncodingObserver.get_obs(lane) in every env (draws in
+        call order): writes and returns obs[:, lane]."""
+        self.component(_abi.GW_OP_OBSERVE, lane, obs=self.obs)
+        return self.obs[:, lane]
+
     def rollout_buffers(self, n_steps):
         """Per-step output slabs for rollout(): obs[n][E][A][...], reward[n][E][A],
         done[n][E][A], all_done[n][E]."""

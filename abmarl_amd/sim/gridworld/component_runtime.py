@@ -1,0 +1,182 @@
+"""The component plugin API on the engine (gw_component).
+
+The reference composes a simulation's step() from component calls
+(PositionState.reset, MoveActor.process_action, BinaryAttackActor /
+SelectiveAttackActor.process_action, PositionCenteredEncodingObserver.get_obs;
+state.py:13-22, actor.py:13-52, observer.py:13-52).  Here each such call is
+one device operation on a one-env engine: a wave loads the env, runs the
+component's body exactly as the fused programs do (same MT19937 stream
+consumption), and stores it back.
+
+The Python objects stay the reference's: the agents' position / health /
+active, the Grid's insertion-ordered cells (grid.py) and the global numpy
+legacy RNG.  Before every operation the runtime uploads them (in-cell order
+becomes the engine's per-entity placement sequence), after it the engine's
+results are mirrored back, so user code may read or edit either between
+calls, and a user-written step() runs its component calls on the GPU in its
+own order.  The done components are plain reads of that state and run on the
+host (components.py).
+
+One runtime per (grid, agents dict); it is rebuilt when the agents'
+attributes or the grid's overlapping change.  The components' own parameters
+(no_overlap_at_reset, stacked_attacks, attack_mapping, observe_self) travel
+with each call, so several actors / observers may share a grid, as in the
+reference's tests.  Limit: the one-wave engine (at most 64 entities).
+"""
+import numpy as np
+import torch
+
+from abmarl_amd import _abi
+from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent
+
+
+class ComponentError(RuntimeError):
+    pass
+
+
+def _registry(grid):
+    return grid.__dict__.setdefault('_components', [])
+
+
+def register_component(component):
+    """Called by the engine-backed components at construction."""
+    reg = _registry(component.grid)
+    if component not in reg:
+        reg.append(component)
+
+
+class ComponentRuntime:
+    @staticmethod
+    def of(component):
+        grid, agents = component.grid, component.agents
+        rts = grid.__dict__.setdefault('_component_runtimes', {})
+        sig = ComponentRuntime._signature(grid, agents)
+        rt = rts.get(id(agents))
+        if rt is None or rt.agents is not agents or rt.sig != sig:
+            rt = rts[id(agents)] = ComponentRuntime(grid, agents, sig)
+        return rt
+
+    @staticmethod
+    def _signature(grid, agents):
+        from abmarl_amd.sim.gridworld.components import SelectiveAttackActor
+        sig = [tuple(agents), tuple(sorted(grid.overlap_bits().items())),
+               any(isinstance(c, SelectiveAttackActor) and c.agents is agents for c in _registry(grid))]
+        sig.append(tuple((a.encoding, getattr(a, 'view_range', None), getattr(a, 'move_range', None),
+                          getattr(a, 'attack_range', None), getattr(a, 'attack_strength', None),
+                          getattr(a, 'attack_accuracy', None), getattr(a, 'simultaneous_attacks', None),
+                          getattr(a, 'initial_health', None),
+                          None if a.initial_position is None else tuple(a.initial_position), a.blocking)
+                         for a in agents.values()))
+        return tuple(sig)
+
+    def __init__(self, grid, agents, sig):
+        from abmarl_amd.engine import GridWorldEngine
+        from abmarl_amd.sim.gridworld.compile import agent_spec
+        self.grid, self.agents, self.sig = grid, agents, sig
+        self.ids = list(agents)
+        self.index = {aid: i for i, aid in enumerate(self.ids)}
+        if len(self.ids) > 64:
+            raise ComponentError("the component runtime holds at most 64 entities per grid")
+        # selective actions need the (2r+1)^2 action row; binary uses args[2] only
+        kind = _abi.GW_ATTACK_SELECTIVE if sig[2] else _abi.GW_ATTACK_BINARY
+        views = [a.view_range for a in agents.values() if isinstance(a, GridObservingAgent)]
+        cc = _abi.CompiledConfig(
+            grid.rows, grid.cols, [agent_spec(a) for a in agents.values()], _abi.GW_SIM_TEAM_BATTLE,
+            grid.overlap_bits(), {}, done_kind=_abi.GW_DONE_ACTIVE,
+            obs_range=max(views) if views else 0, attack_kind=kind)
+        cc.cfg.all_lanes = 1
+        self.cc = cc
+        self.eng = GridWorldEngine(cc, 1, seeds=[0])
+        self.dev = self.eng.device
+        assert list(self.eng.lane_entities) == list(range(len(self.ids)))
+        A = len(self.ids)
+        self.result = torch.zeros((1, 2 + A), dtype=torch.int32, device=self.dev)
+        self.args = torch.zeros((1, self.eng.act_dim), dtype=torch.int32, device=self.dev)
+        self.obs = torch.full((1, A) + self.eng.obs_shape, -2, dtype=torch.int32, device=self.dev)
+
+    # ------------------------------------------------------------- sync
+    def _upload(self):
+        A = len(self.ids)
+        pos = np.zeros((1, A, 2), np.int32)
+        health = np.zeros((1, A), np.float64)
+        flags = np.zeros((1, A), np.uint8)
+        seq = np.zeros((1, A), np.int32)
+        cells = self.grid._internal
+        order = {}
+        if any(cells[r, c] for r in range(self.grid.rows) for c in range(self.grid.cols)):
+            k = 0
+            for r in range(self.grid.rows):
+                for c in range(self.grid.cols):
+                    for aid in (cells[r, c] or {}):
+                        order[aid] = (k, r, c)
+                        k += 1
+        for i, (aid, a) in enumerate(self.agents.items()):
+            if a.position is not None:
+                pos[0, i] = a.position
+            f = _abi.FLAG_LIVE
+            if aid in order:
+                seq[0, i] = order[aid][0]
+                pos[0, i] = order[aid][1:]
+                f |= _abi.FLAG_IN_GRID
+            if a.active:
+                f |= _abi.FLAG_ACTIVE
+            flags[0, i] = f
+            if isinstance(a, HealthAgent) and a.health is not None:
+                health[0, i] = a.health
+        st = np.random.get_state()
+        assert st[0] == 'MT19937'
+        self._gauss = st[3:]
+        mt = np.zeros((1, _abi.GW_MT_STRIDE), np.uint32)
+        mt[0, :624] = st[1]
+        mt[0, 624] = st[2]
+        mt[0, 625] = A                      # next placement sequence number
+        d = self.dev
+        self.eng.set_state(pos=torch.as_tensor(pos, device=d), health=torch.as_tensor(health, device=d),
+                           flags=torch.as_tensor(flags, device=d), seq=torch.as_tensor(seq, device=d),
+                           mt=torch.as_tensor(mt.view(np.int32), device=d))
+
+    def _download(self, op):
+        st = {k: v.cpu().numpy() for k, v in self.eng.get_state().items()}
+        mt = st['mt'].view(np.uint32)[0]
+        np.random.set_state(('MT19937', mt[:624].copy(), int(mt[624])) + tuple(self._gauss))
+        flags = st['flags'][0]
+        in_grid = []
+        for i, (aid, a) in enumerate(self.agents.items()):
+            inside = bool(flags[i] & _abi.FLAG_IN_GRID)
+            if inside or a.position is not None:
+                a.position = st['pos'][0, i].astype(int)
+            if isinstance(a, HealthAgent) and (a.health is not None or op == _abi.GW_OP_HEALTH_RESET):
+                a._health = float(st['health'][0, i])
+            a._active = bool(flags[i] & _abi.FLAG_ACTIVE)
+            if inside:
+                in_grid.append((int(st['seq'][0, i]), aid, a))
+        cells = self.grid._internal
+        if op == _abi.GW_OP_POSITION_RESET or any(cells[r, c] is not None for r in range(self.grid.rows)
+                         for c in range(self.grid.cols)):
+            self.grid.reset()
+            for _, aid, a in sorted(in_grid, key=lambda x: x[0]):
+                cells[tuple(a.position)][aid] = a
+
+    # ----------------------------------------------------------- operations
+    def op(self, op, agent=None, args=None):
+        """Run one component operation; returns (status, attacked agents, err)."""
+        lane = -1 if agent is None else self.index[agent.id]
+        self._upload()
+        if args is not None:
+            a = np.zeros((1, self.eng.act_dim), np.int32)
+            flat = np.asarray(args, dtype=np.int64).reshape(-1)
+            a[0, :flat.size] = flat
+            self.args.copy_(torch.as_tensor(a, device=self.dev))
+        self.eng.err.zero_()
+        self.eng.component(op, lane, self.args if args is not None else None, self.result,
+                           self.obs if op == _abi.GW_OP_OBSERVE else None)
+        res = self.result[0].cpu().numpy()
+        err = int(self.eng.err[0].item())
+        self._download(op)
+        attacked = [self.agents[self.ids[int(x)]] for x in res[2:2 + int(res[1])]]
+        return int(res[0]), attacked, err
+
+    def observe(self, agent, observe_self=True):
+        self.op(_abi.GW_OP_OBSERVE, agent, [int(observe_self)])
+        d = 2 * agent.view_range + 1
+        return self.obs[0, self.index[agent.id], :d, :d].cpu().numpy().astype(int)

@@ -1,9 +1,15 @@
 """State / Actor / Observer / Done components (the reference's plugin API).
 
 Each class keeps the reference's name, constructor arguments, validation and
-space assignment; its per-agent Python body is executed by the engine's
-fused HIP step instead of here.  What each one contributes to the compiled
-engine configuration is in ``abmarl_amd/sim/gridworld/compile.py``.
+space assignment.  They run on the engine two ways:
+  * as descriptors of the fused step programs (TeamBattleSim, ...): what each
+    one contributes to the compiled configuration is in compile.py;
+  * called directly, as the reference's components are by a user-written
+    step(): PositionState / HealthState.reset, MoveActor / BinaryAttackActor /
+    SelectiveAttackActor.process_action and PositionCenteredEncodingObserver
+    .get_obs are device operations (gw_component, component_runtime.py) on
+    the agents and the Grid they were built with; the done components read
+    that state.
 
 Reference: abmarl/sim/gridworld/state.py:13-166,622-641; actor.py:13-114,
 237-501; observer.py:13-52,153-250; done.py:10-153.
@@ -12,8 +18,10 @@ from abc import ABC, abstractmethod
 
 import numpy as np
 
+from abmarl_amd import _abi
 from abmarl_amd.spaces import Box, Discrete
 from abmarl_amd.sim.gridworld.base import GridWorldBaseComponent
+from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime, register_component
 from abmarl_amd.sim.gridworld.agent import (
     GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, OrientationAgent)
 
@@ -44,10 +52,31 @@ class PositionState(StateBaseComponent):
             "Randomize placement order must be True or False."
         self.no_overlap_at_reset = no_overlap_at_reset
         self.randomize_placement_order = randomize_placement_order
+        register_component(self)
+
+    def reset(self, **kwargs):
+        """Grid.reset, then every agent placed (gw_component POSITION_RESET)."""
+        if self.randomize_placement_order:
+            raise NotImplementedError("randomize_placement_order (Python random.shuffle) is not "
+                                      "reproduced by the engine")
+        status, _, err = ComponentRuntime.of(self).op(
+            _abi.GW_OP_POSITION_RESET, args=[int(self.no_overlap_at_reset)])
+        if err & _abi.GW_ERR_INIT_POSITION:
+            raise AssertionError("Cell is not available for an agent with an initial position.")
+        if err & _abi.GW_ERR_NO_CELL or not status:
+            raise RuntimeError("Could not find a cell for an agent")
 
 
 class HealthState(StateBaseComponent):
     """state.py:622-641: initial_health or np.random.uniform(0, 1)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        register_component(self)
+
+    def reset(self, **kwargs):
+        """gw_component HEALTH_RESET."""
+        ComponentRuntime.of(self).op(_abi.GW_OP_HEALTH_RESET)
 
 
 class OrientationState(StateBaseComponent):
@@ -81,6 +110,18 @@ class MoveActor(ActorBaseComponent):
             if isinstance(agent, self.supported_agent_type):
                 agent.action_space[self.key] = Box(-agent.move_range, agent.move_range, (2,), int)
                 agent.null_action[self.key] = np.zeros((2,), dtype=int)
+        register_component(self)
+
+    def process_action(self, agent, action_dict, **kwargs):
+        """True if the move succeeded (gw_component MOVE); None for agents that
+        are not MovingAgents (actor.py:82-114)."""
+        if not isinstance(agent, self.supported_agent_type):
+            return None
+        status, _, err = ComponentRuntime.of(self).op(_abi.GW_OP_MOVE, agent,
+                                                      np.asarray(action_dict[self.key]).reshape(2))
+        if err & _abi.GW_ERR_NOT_IN_GRID:
+            raise KeyError(agent.id)                  # Grid.remove of an agent not in its cell
+        return bool(status)
 
     @property
     def key(self):
@@ -132,6 +173,26 @@ class AttackActorBaseComponent(ActorBaseComponent, ABC):
         for agent in self.agents.values():
             if isinstance(agent, self.supported_agent_type):
                 self._assign_space(agent)
+        register_component(self)
+
+    def process_action(self, attacking_agent, action_dict, **kwargs):
+        """(attack_status, attacked_agents) as actor.py:306-361: (False, []) when
+        not attempted, (True, []) when it failed; damage is applied and killed
+        agents leave the grid (gw_component ATTACK)."""
+        if not isinstance(attacking_agent, self.supported_agent_type):
+            return False, []
+        # this actor's parameters travel with the call: stacked | selective, the
+        # attacker's attack_mapping entry as an encoding bitmask
+        flags = int(self.stacked_attacks) | (2 if isinstance(self, SelectiveAttackActor) else 0)
+        amap = sum(1 << e for e in self.attack_mapping.get(attacking_agent.encoding, ())
+                   if 1 <= e <= _abi.GW_MAX_ENC)
+        status, attacked, _ = ComponentRuntime.of(self).op(
+            _abi.GW_OP_ATTACK, attacking_agent,
+            [flags, amap] + list(self._attack_args(action_dict[self.key])))
+        return bool(status), attacked
+
+    def _attack_args(self, action):
+        return np.asarray(action, dtype=np.int64).reshape(-1)
 
     @property
     def key(self):
@@ -194,6 +255,15 @@ class PositionCenteredEncodingObserver(ObserverBaseComponent):
                 side = agent.view_range * 2 + 1
                 agent.observation_space[self.key] = Box(-2, max_encoding, (side, side), int)
                 agent.null_observation[self.key] = -2 * np.ones((side, side), dtype=int)
+        register_component(self)
+
+    def get_obs(self, agent, **kwargs):
+        """The agent's (2v+1)^2 window (gw_component OBSERVE; crowded cells
+        draw np.random.choice in the reference's order); {} for agents that
+        are not GridObservingAgents (observer.py:204-250)."""
+        if not isinstance(agent, self.supported_agent_type):
+            return {}
+        return {self.key: ComponentRuntime.of(self).observe(agent, self.observe_self)}
 
     @property
     def key(self):
@@ -240,9 +310,18 @@ class DoneBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
 class ActiveDone(DoneBaseComponent):
     """done.py:39-56: done = not active; all done = no active agent."""
 
+    def get_done(self, agent, **kwargs):
+        return not agent.active
+
+    def get_all_done(self, **kwargs):
+        return not any(agent.active for agent in self.agents.values())
+
 
 class OneTeamRemainingDone(ActiveDone):
     """done.py:140-153: all done when the active agents share <= 1 encoding."""
+
+    def get_all_done(self, **kwargs):
+        return len({agent.encoding for agent in self.agents.values() if agent.active}) <= 1
 
 
 class _TargetMappingDone(DoneBaseComponent):
@@ -274,7 +353,19 @@ class TargetAgentDone(_TargetMappingDone):
     """done.py:59-99: an agent is done when it is on its target's position
     (np.array_equal of the positions); all done when every mapped agent is."""
 
+    def get_done(self, agent, **kwargs):
+        return np.array_equal(agent.position, self.agents[self.target_mapping[agent.id]].position)
+
+    def get_all_done(self, **kwargs):
+        return all(self.get_done(self.agents[aid]) for aid in self.target_mapping)
+
 
 class TargetDestroyedDone(_TargetMappingDone):
     """done.py:102-137: an agent is done when its target is inactive; all
     done when every mapped agent's target is."""
+
+    def get_done(self, agent, **kwargs):
+        return not self.agents[self.target_mapping[agent.id]].active
+
+    def get_all_done(self, **kwargs):
+        return all(self.get_done(self.agents[aid]) for aid in self.target_mapping)

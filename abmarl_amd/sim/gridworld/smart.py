@@ -7,8 +7,12 @@ order in which PositionState and HealthState draw from the RNG at reset is
 set-iteration order there; here it is pinned by ``state_order``
 ('position_health' by default, or 'health_position').
 
-Runtime: the simulation compiles itself to a ``gw_config`` and runs on a
-one-env ``GridWorldEngine``.  The engine fuses the AllStepManager protocol
+Runtime (a subclass that names an engine program, ``_engine_program``): the
+simulation compiles itself to a ``gw_config`` and runs on a one-env
+``GridWorldEngine``.  A subclass with its own step() and no engine program
+(a user-written simulation) runs as the reference's smart.py does: reset /
+get_obs / get_done / get_all_done iterate its components, and each
+component call is a device operation (component_runtime.py).  The engine fuses the AllStepManager protocol
 (step -> obs -> rewards -> dones -> done_agents, all_step_manager.py:51-95)
 into one kernel, so ``step`` computes every live agent's observation, reward
 and done at once and ``get_obs`` / ``get_reward`` / ``get_done`` return those
@@ -91,27 +95,50 @@ class SmartGridWorldSimulation(GridWorldSimulation, ABC):
         return self._runtime
 
     # ------------------------------------------------------------ ABS API
+    # (no engine program: the component path, smart.py:86-117 with every
+    # component call on the device)
     def reset(self, **kwargs):
         assert self._states, "Smart Simulation requires '_states' attribute."
-        self._rt().reset()
+        if self._engine_program is None:
+            # the reference iterates a set (smart.py:37); state_order pins it
+            first = 'PositionState' if self.state_order == 'position_health' else 'HealthState'
+            for state in sorted(self._states, key=lambda s: type(s).__name__ != first):
+                state.reset(**kwargs)
+        else:
+            self._rt().reset()
         self.rewards = {a.id: 0 for a in self.agents.values() if isinstance(a, Agent)}
 
     def step(self, action_dict, **kwargs):
+        assert self._engine_program is not None, \
+            f"{type(self).__name__} has no engine program: implement step() with its components"
         self._rt().step(action_dict)
 
     def get_obs(self, agent_id, **kwargs):
         assert self._observers, "Smart Simulation requires '_observers' attribute."
+        if self._engine_program is None:
+            agent = self.agents[agent_id]
+            return {k: v for observer in self._observers
+                    for k, v in observer.get_obs(agent, **kwargs).items()}
         return self._rt().get_obs(agent_id)
 
     def get_reward(self, agent_id, **kwargs):
+        if self._engine_program is None:
+            reward = self.rewards[agent_id]
+            self.rewards[agent_id] = 0
+            return reward
         return self._rt().get_reward(agent_id)
 
     def get_done(self, agent_id, **kwargs):
         assert self._dones, "Smart Simulation requires '_dones' attribute."
+        if self._engine_program is None:
+            agent = self.agents[agent_id]
+            return all(done.get_done(agent, **kwargs) for done in self._dones)
         return self._rt().get_done(agent_id)
 
     def get_all_done(self, **kwargs):
         assert self._dones, "Smart Simulation requires '_dones' attribute."
+        if self._engine_program is None:
+            return all(done.get_all_done(**kwargs) for done in self._dones)
         return self._rt().get_all_done()
 
     def get_info(self, agent_id, **kwargs):
@@ -121,3 +148,4 @@ class SmartGridWorldSimulation(GridWorldSimulation, ABC):
     def done_agents(self):
         """Agents the fused manager protocol considers done."""
         return self._rt().done_agents()
+

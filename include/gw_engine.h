@@ -99,6 +99,9 @@ typedef int32_t gw_status;
 #define GW_ERR_TUNNEL_PLACE   8u  /* Pacman: Grid.place at the far end of the tunnel refused the
                                      agent, which is left off the grid (pacman.py:88-93);
                                      its next move would raise KeyError in Grid.remove */
+#define GW_ERR_NOT_IN_GRID   16u  /* gw_component MOVE of an entity that is not in the grid:
+                                     Grid.remove raises KeyError (actor.py:108-110);
+                                     the entity stays where it was                    */
 
 /* ------------------------------------------------------------ agent kinds */
 /* bit flags describing which reference mixins an entity derives from        */
@@ -203,6 +206,9 @@ typedef struct gw_config {
        before this step, non-observers): steady-state obs stores shrink with
        the done fraction.  0: every row is written every call.              */
     int32_t  persistent_obs;
+    /* 1: every entity is a lane (no static entities in the cell template):
+       the component plugin API keeps all entity state in lanes              */
+    int32_t  all_lanes;
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack
@@ -302,6 +308,42 @@ gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
    the reference; it is the benchmark's synthetic policy.                     */
 gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t env_offset,
                             int32_t* actions, void* stream);
+
+/* ---------------------------------------------------------------------
+ * The component plugin API (ActorBaseComponent.process_action, actor.py:13-52;
+ * ObserverBaseComponent.get_obs, observer.py:13-52; StateBaseComponent.reset,
+ * state.py:13-22) as device operations: ONE component call for one entity
+ * (lane) in every env, on the engine's state (positions, health, active,
+ * in-grid, in-cell order, the MT19937 stream), so that a step() composed of
+ * component calls in Python runs them on the GPU in its own order.  The
+ * one-wave engine only (GW_KERNEL_WAVE).
+ *   GW_OP_POSITION_RESET  PositionState.reset (state.py:88-166): every cell
+ *                         emptied, every entity placed again; args[e][0] =
+ *                         no_overlap_at_reset (NULL args: the config's)
+ *   GW_OP_HEALTH_RESET    HealthState.reset (state.py:629-641)
+ *   GW_OP_MOVE            MoveActor.process_action(lane, {'move': args[e][0:2]})
+ *   GW_OP_ATTACK          an attack actor's process_action(lane, {'attack':
+ *                         args[e][2] (binary) or args[e][2:] (selective cells)});
+ *                         args[e][0] = stacked_attacks | 2 (SelectiveAttackActor),
+ *                         args[e][1] = attack_mapping[the attacker's encoding] bits
+ *   GW_OP_OBSERVE         PositionCenteredEncodingObserver.get_obs(lane): writes
+ *                         obs[e][lane] only (draws in call order); args[e][0] =
+ *                         observe_self (NULL args: the config's)
+ *   The components' own parameters travel with each call, so several actors
+ *   or observers with different parameters may share one handle.
+ *   args     device int32[E][gw_act_dim(h)]
+ *   result   device int32[E][2 + A] or NULL: [0] status (MOVE 1 True, 0 False,
+ *            -1 None for a non-MovingAgent; ATTACK 1 attempted, 0 not; resets 1
+ *            placed, 0 raised), [1] n attacked, [2..] attacked lanes in list order
+ *   obs      device int32[E][A][S][S] (OBSERVE)
+ *   err_flags device uint32[E] or NULL (|= GW_ERR_*)                          */
+#define GW_OP_POSITION_RESET 1
+#define GW_OP_HEALTH_RESET   2
+#define GW_OP_MOVE           3
+#define GW_OP_ATTACK         4
+#define GW_OP_OBSERVE        5
+gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
+                       int32_t* obs, uint32_t* err_flags, void* stream);
 
 /* A fragment of n_steps consecutive AllStepManager steps with auto-reset
    (1 SAME_STEP, 2 NEXT_STEP) in one call: the same results as n_steps

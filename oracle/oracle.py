@@ -16,11 +16,17 @@ LIB = os.path.join(HERE, 'build', 'libgw_oracle.so')
 
 
 def build(force=False):
+    """(Re)build under an exclusive file lock, so parallel test workers
+    never load a half-written or stale library."""
+    import fcntl
     srcs = [os.path.join(HERE, 'gw_oracle.c'),
             os.path.join(os.path.dirname(HERE), 'include', 'gw_engine.h')]
-    if force or not os.path.exists(LIB) or \
-            os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
-        subprocess.check_call(['make', '-s', '-C', HERE])
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    with open(LIB + '.lock', 'w') as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if force or not os.path.exists(LIB) or \
+                os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
+            subprocess.check_call(['make', '-s', '-B' if force else '-s', '-C', HERE])
     return LIB
 
 

@@ -90,7 +90,7 @@ def build_traffic(c):
                                                           target_mapping=mapping, **kw)
 
 
-def build_sim(c):
+def build_sim(c, sim_cls=None):
     """The golden case's configuration, built with the host API."""
     if c.get('kind') == 'maze':
         return build_maze(c)
@@ -125,10 +125,10 @@ def build_sim(c):
         for r, cc in c['walls']:
             arr[r, cc] = 'W'
         wenc = c['wall_encoding']
-        return TeamBattleSim.build_sim_from_array(
+        return (sim_cls or TeamBattleSim).build_sim_from_array(
             arr, {'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=wenc, blocking=True)},
             extra_agents=agents, **kwargs)
-    return TeamBattleSim.build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
+    return (sim_cls or TeamBattleSim).build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
 
 
 def team_battle(rows=32, cols=32, n_agents=64, n_teams=2, **kw):

@@ -1,0 +1,508 @@
+"""The component plugin API on the device (gw_component, component_runtime.py).
+
+Two kinds of evidence:
+  * the reference's own component unit tests (tests/sim/gridworld/
+    test_state.py, test_actor.py, test_observer.py in the reference) restated
+    with their scenarios and known answers, every component call running as
+    a gw_component operation on the GPU;
+  * a user-written simulation -- the reference's TeamBattle example step()
+    (examples/sim/team_battle_example.py:33-59) written here against the
+    components, with no engine program -- driven by AllStepManager through
+    the reference's golden trajectories (tests/golden/*.npz), bit-exact in
+    observations, float64 rewards, dones, positions, health, active flags
+    and the numpy MT19937 state after every step.
+
+CPU tests at the bottom cover construction-time validation and that the
+runtime refuses to run without the HIP engine.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from abmarl_amd.sim.gridworld.grid import Grid
+from abmarl_amd.sim.gridworld.agent import (
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
+from abmarl_amd.sim.gridworld.components import (
+    PositionState, HealthState, MoveActor, BinaryAttackActor, SelectiveAttackActor,
+    PositionCenteredEncodingObserver)
+from abmarl_amd.sim.gridworld.smart import SmartGridWorldSimulation
+from abmarl_amd.managers import AllStepManager
+
+gpu = pytest.mark.gpu
+KEY = 'position_centered_encoding'
+
+
+# ------------------------------------------------------------------ states
+@gpu
+def test_position_state_initial_positions():
+    """test_state.py:11-28."""
+    grid = Grid(3, 3)
+    agents = {f'agent{i}': GridWorldAgent(id=f'agent{i}', encoding=1, initial_position=np.array(p))
+              for i, p in enumerate([(0, 1), (1, 2), (2, 0)])}
+    PositionState(grid=grid, agents=agents).reset()
+    for aid, p in zip(agents, [(0, 1), (1, 2), (2, 0)]):
+        np.testing.assert_equal(agents[aid].position, np.array(p))
+        assert grid[p] == {aid: agents[aid]}
+
+
+@gpu
+def test_position_state_no_overlap_at_reset():
+    """test_state.py:31-56: initial positions may overlap, drawn ones may not."""
+    grid = Grid(3, 3, overlapping={1: {1}})
+    init = {3: (2, 2), 8: (0, 0), 9: (0, 0)}
+    agents = {}
+    for i in range(10):
+        kw = dict(initial_position=np.array(init[i])) if i in init else {}
+        agents[f'agent{i}'] = GridWorldAgent(id=f'agent{i}', encoding=1, **kw)
+    PositionState(grid=grid, agents=agents, no_overlap_at_reset=True).reset()
+    assert grid[0, 0] == {'agent8': agents['agent8'], 'agent9': agents['agent9']}
+    assert grid[2, 2] == {'agent3': agents['agent3']}
+    for cell in [(0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (2, 0), (2, 1)]:
+        assert len(grid[cell]) == 1
+
+
+@gpu
+def test_position_state_small_grid():
+    """test_state.py:59-110, including the seed-24 pass / seed-17 failure."""
+    grid = Grid(1, 2, overlapping={1: {1, 2}, 2: {1, 2}, 3: {3}})
+    spec = [(1, (0, 0)), (2, (0, 0)), (3, None), (3, None), (2, None), (1, None)]
+    agents = {f'agent{i}': GridWorldAgent(
+        id=f'agent{i}', encoding=e, **({} if p is None else dict(initial_position=np.array(p))))
+        for i, (e, p) in enumerate(spec)}
+    PositionState(grid=grid, agents=agents).reset()
+    for aid, cell in [('agent0', (0, 0)), ('agent1', (0, 0)), ('agent2', (0, 1)),
+                      ('agent3', (0, 1)), ('agent4', (0, 0)), ('agent5', (0, 0))]:
+        assert aid in grid[cell]
+
+    agents = {'agent0': GridWorldAgent(id='agent0', encoding=1, initial_position=np.array([0, 0])),
+              'agent1': GridWorldAgent(id='agent1', encoding=2, initial_position=np.array([0, 1])),
+              'agent2': GridWorldAgent(id='agent2', encoding=3)}
+    with pytest.raises(RuntimeError):
+        PositionState(grid=grid, agents=agents).reset()
+
+    np.random.seed(24)
+    agents = {'agent0': GridWorldAgent(id='agent0', encoding=1, initial_position=np.array([0, 0])),
+              'agent1': GridWorldAgent(id='agent1', encoding=2),
+              'agent2': GridWorldAgent(id='agent2', encoding=3)}
+    ps = PositionState(grid=grid, agents=agents)
+    ps.reset()
+    assert 'agent0' in grid[0, 0] and 'agent1' in grid[0, 0] and 'agent2' in grid[0, 1]
+    np.random.seed(17)
+    with pytest.raises(RuntimeError):
+        ps.reset()
+
+
+@gpu
+def test_health_state():
+    """test_state.py:113-130 (initial health kept exactly, others uniform(0, 1))."""
+    grid = Grid(3, 3)
+    agents = {'agent0': HealthAgent(id='agent0', encoding=1, initial_health=0.24),
+              'agent1': HealthAgent(id='agent1', encoding=1),
+              'agent2': HealthAgent(id='agent2', encoding=1)}
+    np.random.seed(5)
+    HealthState(agents=agents, grid=grid).reset()
+    assert agents['agent0'].health == 0.24
+    # the two draws are numpy's uniform(0, 1) in agents order
+    np.random.seed(5)
+    expect = np.random.uniform(0, 1, 2)
+    assert [agents['agent1'].health, agents['agent2'].health] == list(expect)
+    assert all(a.active for a in agents.values())
+
+
+# ------------------------------------------------------------------ actors
+@gpu
+def test_move_actor():
+    """test_actor.py:22-78."""
+    grid = Grid(5, 6)
+    spec = [((3, 4), 1, 1), ((2, 2), 2, 2), ((0, 1), 1, 1), ((3, 1), 3, 3)]
+    agents = {f'agent{i}': MovingAgent(id=f'agent{i}', initial_position=np.array(p), encoding=e,
+                                       move_range=r) for i, (p, e, r) in enumerate(spec)}
+    ps = PositionState(grid=grid, agents=agents)
+    move = MoveActor(grid=grid, agents=agents)
+    ps.reset()
+    for moves in ([(1, 1), (-1, 0), (0, 1), (-1, 1)], [(1, 1), (0, 0), (-1, 1), (-1, 0)]):
+        for aid, m in zip(agents, moves):
+            move.process_action(agents[aid], {'move': np.array(m)})
+        for aid, p in zip(agents, [(4, 5), (1, 2), (0, 2), (2, 2)]):
+            np.testing.assert_array_equal(agents[aid].position, np.array(p))
+
+
+@gpu
+def test_move_actor_with_overlap():
+    """test_actor.py:81-131."""
+    grid = Grid(5, 6, overlapping={1: {1}, 2: {3}, 3: {2}})
+    spec = [((4, 4), 1, 1), ((2, 2), 2, 2), ((2, 4), 1, 1), ((3, 2), 3, 3)]
+    agents = {f'agent{i}': MovingAgent(id=f'agent{i}', initial_position=np.array(p), encoding=e,
+                                       move_range=r) for i, (p, e, r) in enumerate(spec)}
+    ps = PositionState(grid=grid, agents=agents)
+    move = MoveActor(grid=grid, agents=agents)
+    ps.reset()
+    rounds = [([(-1, 0), (0, 0), (1, 0), (-1, 0)], [(3, 4), (2, 2), (3, 4), (2, 2)]),
+              ([(-1, 0), (0, 2), (0, -1), (1, 1)], [(2, 4), (2, 2), (3, 3), (2, 2)])]
+    for moves, expect in rounds:
+        for aid, m in zip(agents, moves):
+            move.process_action(agents[aid], {'move': np.array(m)})
+        for aid, p in zip(agents, expect):
+            np.testing.assert_array_equal(agents[aid].position, np.array(p))
+    # the grid container follows the engine: two agents share (2, 2)
+    assert set(grid[2, 2]) == {'agent1', 'agent3'}
+
+
+def _attack_agents(attacker_kw, health=None):
+    h = {} if health is None else dict(initial_health=health)
+    return {
+        'agent0': HealthAgent(id='agent0', initial_position=np.array([4, 4]), encoding=1, **h),
+        'agent1': AttackingAgent(id='agent1', initial_position=np.array([2, 2]), encoding=1,
+                                 attack_range=2, **attacker_kw),
+        'agent2': HealthAgent(id='agent2', initial_position=np.array([2, 3]), encoding=2, **h),
+        'agent3': HealthAgent(id='agent3', initial_position=np.array([3, 2]), encoding=1, **h),
+    }
+
+
+@gpu
+def test_binary_attack_actor():
+    """test_actor.py:454-500."""
+    grid = Grid(5, 6)
+    agents = _attack_agents(dict(attack_strength=1, attack_accuracy=1))
+    ps, hs = PositionState(grid=grid, agents=agents), HealthState(grid=grid, agents=agents)
+    attack = BinaryAttackActor(attack_mapping={1: {1}}, grid=grid, agents=agents)
+    ps.reset()
+    hs.reset()
+    for _ in range(2):
+        status, attacked = attack.process_action(agents['agent1'], {'attack': 1})
+        assert status and attacked
+    assert not agents['agent0'].active and not agents['agent3'].active
+    assert agents['agent0'].health <= 0 and agents['agent3'].health <= 0
+    assert not grid[4, 4] and not grid[3, 2]
+    status, attacked = attack.process_action(agents['agent1'], {'attack': 1})
+    assert status and not attacked
+    assert agents['agent2'].active and agents['agent2'].health > 0 and grid[2, 3]
+
+
+@gpu
+def test_binary_attack_actor_simultaneous_attacks():
+    """test_actor.py:531-591 (attack_strength changed between calls)."""
+    grid = Grid(5, 6)
+    agents = {
+        'agent0': AttackingAgent(id='agent0', initial_position=np.array([2, 2]), encoding=1,
+                                 attack_range=2, attack_strength=0, attack_accuracy=1,
+                                 simultaneous_attacks=3),
+        'agent1': HealthAgent(id='agent1', initial_position=np.array([4, 4]), encoding=1,
+                              initial_health=1),
+        'agent2': HealthAgent(id='agent2', initial_position=np.array([2, 3]), encoding=2,
+                              initial_health=1),
+        'agent3': HealthAgent(id='agent3', initial_position=np.array([3, 2]), encoding=1,
+                              initial_health=1),
+    }
+    ps, hs = PositionState(grid=grid, agents=agents), HealthState(grid=grid, agents=agents)
+    attack = BinaryAttackActor(attack_mapping={1: {1, 2}}, grid=grid, agents=agents)
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 0})
+    assert not status and not attacked
+    for n in (1, 2, 3):
+        status, attacked = attack.process_action(agents['agent0'], {'attack': n})
+        assert status and len(attacked) == n
+    agents['agent0'].attack_strength = 1
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 3})
+    assert status and len(attacked) == 3
+    for aid in ('agent1', 'agent2', 'agent3'):
+        assert not agents[aid].active and agents[aid].health <= 0
+    assert not grid[4, 4] and not grid[2, 3] and not grid[3, 2]
+
+
+@gpu
+def test_binary_attack_actor_stacked_attack():
+    """test_actor.py:649-721: two actors with different mappings / stacking on one grid."""
+    grid = Grid(5, 6)
+    agents = {
+        'agent0': AttackingAgent(id='agent0', initial_position=np.array([2, 2]), encoding=1,
+                                 attack_range=2, attack_strength=1, attack_accuracy=1,
+                                 simultaneous_attacks=2),
+        'agent1': HealthAgent(id='agent1', initial_position=np.array([4, 4]), encoding=1,
+                              initial_health=1),
+        'agent2': HealthAgent(id='agent2', initial_position=np.array([2, 3]), encoding=2,
+                              initial_health=1),
+        'agent3': HealthAgent(id='agent3', initial_position=np.array([3, 2]), encoding=1,
+                              initial_health=1),
+    }
+    ps, hs = PositionState(grid=grid, agents=agents), HealthState(grid=grid, agents=agents)
+    attack = BinaryAttackActor(attack_mapping={1: {1}}, stacked_attacks=False, grid=grid,
+                               agents=agents)
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 2})
+    assert status and len(attacked) == 2
+    assert agents['agent1'] in attacked and agents['agent3'] in attacked
+    assert agents['agent2'] not in attacked
+    assert not agents['agent1'].active and not agents['agent3'].active
+    assert not grid[4, 4] and not grid[3, 2]
+
+    agents['agent0'].attack_strength = 0.5
+    attack = BinaryAttackActor(attack_mapping={1: {2}}, stacked_attacks=True, grid=grid,
+                               agents=agents)
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 1})
+    assert status and attacked == [agents['agent2']]
+    assert agents['agent2'].health == 0.5
+    agents['agent0'].attack_strength = 0
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 2})
+    assert status and len(attacked) == 2 and attacked[0] == attacked[1]
+    assert agents['agent2'].health == 0.5
+    agents['agent0'].attack_strength = 0.25
+    status, attacked = attack.process_action(agents['agent0'], {'attack': 2})
+    assert status and len(attacked) == 2 and attacked[0] == attacked[1]
+    assert not agents['agent2'].active and agents['agent2'].health <= 0
+    assert not grid[2, 3]
+
+
+def _cells(*hits, fill=0):
+    a = np.full((5, 5), fill, dtype=int)
+    for r, c in hits:
+        a[r, c] = 1 - fill
+    return {'attack': a}
+
+
+@gpu
+def test_selective_attack_actor():
+    """test_actor.py:724-882 (attacked lists in the reference's cell order)."""
+    grid = Grid(5, 6)
+    agents = _attack_agents(dict(attack_strength=1, attack_accuracy=1))
+    ps, hs = PositionState(grid=grid, agents=agents), HealthState(grid=grid, agents=agents)
+    attack = SelectiveAttackActor(attack_mapping={1: {1}}, grid=grid, agents=agents)
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent1'], _cells((4, 4)))
+    assert status and attacked == [agents['agent0']]
+    assert not agents['agent0'].active and agents['agent0'].health <= 0 and not grid[4, 4]
+    status, attacked = attack.process_action(agents['agent1'], _cells((3, 2)))
+    assert status and attacked == [agents['agent3']]
+    assert not agents['agent3'].active and not grid[3, 2]
+
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent1'], _cells((3, 2), (4, 4)))
+    assert status and attacked == [agents['agent3'], agents['agent0']]
+    assert not grid[4, 4] and not grid[3, 2]
+
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent1'], _cells((3, 2), (4, 4), fill=1))
+    assert status and not attacked
+    assert all(a.active for a in agents.values())
+    assert grid[4, 4] and grid[3, 2] and grid[2, 2] and grid[2, 3]
+    status, attacked = attack.process_action(agents['agent1'], _cells(fill=1))
+    assert status and attacked == [agents['agent3'], agents['agent0']]
+    assert agents['agent1'].active and agents['agent2'].active
+    assert not grid[4, 4] and not grid[3, 2] and grid[2, 2] and grid[2, 3]
+
+    ps.reset()
+    hs.reset()
+    status, attacked = attack.process_action(agents['agent1'], _cells())
+    assert not status and not attacked
+    assert all(a.active for a in agents.values())
+
+
+# --------------------------------------------------------------- observers
+def _observer_agents(blocking):
+    return {
+        'agent0': GridObservingAgent(id='agent0', encoding=1, view_range=2,
+                                     initial_position=np.array([2, 2])),
+        'agent1': GridObservingAgent(id='agent1', encoding=2, view_range=1,
+                                     initial_position=np.array([0, 0])),
+        'agent2': GridObservingAgent(id='agent2', encoding=3, view_range=4,
+                                     initial_position=np.array([4, 4])),
+        'agent3': GridWorldAgent(id='agent3', encoding=5, initial_position=np.array([3, 3]),
+                                 blocking=blocking),
+        'agent4': GridWorldAgent(id='agent4', encoding=4, initial_position=np.array([1, 1]),
+                                 blocking=blocking),
+        'agent5': GridWorldAgent(id='agent5', encoding=6, initial_position=np.array([2, 1]),
+                                 blocking=blocking),
+    }
+
+
+N = -1
+OUT9 = [[N] * 9] * 4
+
+
+@gpu
+@pytest.mark.parametrize('blocking', [False, True])
+def test_position_centered_observer(blocking):
+    """test_observer.py:194-339: views 2, 1 and 4 on one grid, with and
+    without blocking walls."""
+    grid = Grid(5, 5)
+    agents = _observer_agents(blocking)
+    ps = PositionState(grid=grid, agents=agents)
+    observer = PositionCenteredEncodingObserver(agents=agents, grid=grid)
+    ps.reset()
+    if not blocking:
+        e0 = [[2, 0, 0, 0, 0], [0, 4, 0, 0, 0], [0, 6, 1, 0, 0], [0, 0, 0, 5, 0], [0, 0, 0, 0, 3]]
+        e2 = [r + [N] * 4 for r in e0] + OUT9
+    else:
+        e0 = [[-2, -2, 0, 0, 0], [-2, 4, 0, 0, 0], [-2, 6, 1, 0, 0], [-2, 0, 0, 5, -2],
+              [0, 0, 0, -2, -2]]
+        e2 = [r + [N] * 4 for r in [[-2, -2, -2, 0, 0], [-2, -2, -2, 0, 0], [-2, -2, -2, -2, 0],
+                                    [0, 0, -2, 5, 0], [0, 0, 0, 0, 3]]] + OUT9
+    e1 = [[N, N, N], [N, 2, 0], [N, 0, 4]]
+    for aid, expect in (('agent0', e0), ('agent1', e1), ('agent2', e2)):
+        np.testing.assert_array_equal(observer.get_obs(agents[aid])[KEY], np.array(expect))
+    assert observer.get_obs(agents['agent3']) == {}
+
+
+@gpu
+def test_observe_self():
+    """test_observer.py:844-903: two observers (observe_self True / False)
+    sharing one grid, seed 24, two agents on one cell."""
+    np.random.seed(24)
+
+    class HackAgent(GridObservingAgent, MovingAgent):
+        pass
+
+    agents = {
+        'agent0': GridObservingAgent(id='agent0', encoding=1, view_range=2,
+                                     initial_position=np.array([2, 2])),
+        'agent1': GridObservingAgent(id='agent1', encoding=2, view_range=1,
+                                     initial_position=np.array([0, 0])),
+        'agent2': HackAgent(id='agent2', encoding=2, view_range=1,
+                            initial_position=np.array([2, 2]), move_range=1),
+    }
+    grid = Grid(5, 5, overlapping={1: {2}, 2: {1}})
+    PositionState(grid=grid, agents=agents).reset()
+    self_obs = PositionCenteredEncodingObserver(agents=agents, grid=grid)
+    no_self = PositionCenteredEncodingObserver(agents=agents, grid=grid, observe_self=False)
+    z5 = np.zeros((5, 5), int)
+    e = z5.copy(); e[0, 0] = 2; e[2, 2] = 1
+    np.testing.assert_array_equal(self_obs.get_obs(agents['agent0'])[KEY], e)
+    e[2, 2] = 2
+    np.testing.assert_array_equal(no_self.get_obs(agents['agent0'])[KEY], e)
+    np.testing.assert_array_equal(self_obs.get_obs(agents['agent1'])[KEY],
+                                  np.array([[N, N, N], [N, 2, 0], [N, 0, 0]]))
+    np.testing.assert_array_equal(no_self.get_obs(agents['agent1'])[KEY],
+                                  np.array([[N, N, N], [N, 0, 0], [N, 0, 0]]))
+
+
+# ------------------------------------------- a user-written step() on the API
+class UserTeamBattle(SmartGridWorldSimulation):
+    """The reference's TeamBattle example (team_battle_example.py:23-59) as a
+    user would write it: no engine program, its step() composed from the
+    components; every component call is a device operation."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.move_actor = MoveActor(**kwargs)
+        self.attack_actor = BinaryAttackActor(**kwargs)
+        self.finalize()
+
+    def step(self, action_dict, **kwargs):
+        for agent_id, action in action_dict.items():
+            agent = self.agents[agent_id]
+            if agent.active:
+                status, attacked = self.attack_actor.process_action(agent, action, **kwargs)
+                if status:
+                    if not attacked:
+                        self.rewards[agent_id] -= 0.1
+                    else:
+                        for other in attacked:
+                            if not other.active:
+                                self.rewards[other.id] -= 1
+                                self.rewards[agent_id] += 1
+        for agent_id, action in action_dict.items():
+            agent = self.agents[agent_id]
+            if agent.active:
+                if not self.move_actor.process_action(agent, action, **kwargs):
+                    self.rewards[agent.id] -= 0.1
+        for agent_id in action_dict:
+            self.rewards[agent_id] -= 0.01
+
+
+def _obs_array(obs, ids, S):
+    out = np.full((len(ids), S, S), -2, dtype=np.int64)
+    for i, aid in enumerate(ids):
+        o = obs.get(aid, {}).get(KEY)
+        if o is not None:
+            out[i, :o.shape[0], :o.shape[1]] = o
+    return out
+
+
+USER_CASES = [('tb_small', 40, 3), ('tb_order', 30, 2), ('tb_walls', 30, 2),
+              ('tb_destroy', 30, 2), ('tb_chase', 30, 2), ('tb_views', 25, 2)]
+
+
+@gpu
+@pytest.mark.parametrize('name,steps,envs', USER_CASES)
+def test_user_step_replays_reference(name, steps, envs):
+    """AllStepManager(UserTeamBattle) replays the reference's golden
+    trajectories, one env at a time, bit-exactly."""
+    from tests.cases import load_golden, build_sim
+    g = load_golden(name)
+    c = g['case']
+    S = g['obs0'].shape[-1]
+    for e in range(envs):
+        sim = build_sim(c, sim_cls=UserTeamBattle)
+        assert sim._engine_program is None
+        m = AllStepManager(sim)
+        ids = list(m.agents)
+        np.random.seed(c['seeds'][e])
+        obs = m.reset()
+        np.testing.assert_array_equal(_obs_array(obs, ids, S), g['obs0'][e], err_msg='reset obs')
+        for t in range(steps):
+            acts = {aid: {'move': g['actions'][t, e, i, :2].astype(int),
+                          'attack': int(g['actions'][t, e, i, 2])}
+                    for i, aid in enumerate(ids) if aid not in m.done_agents}
+            obs, rew, done, _ = m.step(acts)
+            where = f'{name} env {e} step {t}'
+            np.testing.assert_array_equal(_obs_array(obs, ids, S), g['obs'][t, e], err_msg=where)
+            for i, aid in enumerate(ids):
+                if aid in rew:
+                    assert np.float64(rew[aid]).view(np.uint64) == \
+                        np.float64(g['reward'][t, e, i]).view(np.uint64), where
+                    assert int(bool(done[aid])) == g['done'][t, e, i], where
+                a = m.agents[aid]
+                assert tuple(a.position) == tuple(g['pos'][t, e, i]), where
+                assert getattr(a, 'health', 0.0) == g['health'][t, e, i], where
+                assert int(a.active) == g['active'][t, e, i], where
+            assert int(bool(done['__all__'])) == g['all_done'][t, e], where
+            st = np.random.get_state()
+            assert st[2] == g['mt_pos'][t, e], where
+            assert zlib.crc32(np.ascontiguousarray(st[1], dtype=np.uint32).tobytes()) == \
+                int(g['mt_crc'][t, e]), where
+            if g['reset_mask'][t, e]:
+                obs = m.reset()
+                np.testing.assert_array_equal(_obs_array(obs, ids, S), g['reset_obs'][t, e],
+                                              err_msg=where + ' reset')
+
+
+# -------------------------------------------------------------------- CPU
+def test_attack_mapping_validation():
+    """test_actor.py:503-528: malformed attack mappings are rejected at construction."""
+    grid = Grid(5, 6)
+    agents = _attack_agents(dict(attack_strength=1, attack_accuracy=1))
+    for bad in ([1, 2, 3], {'1': {3}, 2.0: {6}}, {1: 3, 2: [6]}, {1: {'2', 3}, 2: {2, 3}}):
+        with pytest.raises(AssertionError):
+            BinaryAttackActor(agents=agents, grid=grid, attack_mapping=bad)
+
+
+def test_component_spaces():
+    """Action / observation spaces the components assign (test_actor.py:43-46,
+    test_observer.py:216-224)."""
+    from abmarl_amd.spaces import Box, Discrete
+    grid = Grid(5, 5)
+    agents = _observer_agents(False)
+    PositionCenteredEncodingObserver(agents=agents, grid=grid)
+    assert agents['agent0'].observation_space[KEY] == Box(-2, 6, (5, 5), int)
+    assert agents['agent1'].observation_space[KEY] == Box(-2, 6, (3, 3), int)
+    assert agents['agent2'].observation_space[KEY] == Box(-2, 6, (9, 9), int)
+    agents = _attack_agents(dict(attack_strength=1, attack_accuracy=1, simultaneous_attacks=3))
+    BinaryAttackActor(attack_mapping={1: {1}}, grid=Grid(5, 6), agents=agents)
+    assert agents['agent1'].action_space['attack'] == Discrete(4)
+
+
+def test_runtime_needs_the_engine():
+    """The component path has no host fallback: without a GPU it fails."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    grid = Grid(3, 3)
+    agents = {'agent0': GridWorldAgent(id='agent0', encoding=1)}
+    with pytest.raises(Exception):
+        PositionState(grid=grid, agents=agents).reset()
