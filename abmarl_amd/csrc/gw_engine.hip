@@ -2805,17 +2805,34 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // ReachTheTarget runs on a workgroup per env when it has more lanes than a
     // wave (or when the config forces it: the parity tests run the small
     // reference fixtures through it)
-    if (cfg->force_workgroup && !(rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE)) {
-        set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor");
+    // ReachTheTarget (SelectiveAttackActor) and TeamBattle (BinaryAttackActor)
+    // run on a workgroup per env when they have more lanes than a wave (or
+    // when the config forces it: the parity tests run small reference
+    // fixtures through it)
+    const bool tb = cfg->sim_kind == GW_SIM_TEAM_BATTLE;
+    const bool wg_able = (rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE) ||
+                         (tb && cfg->attack_kind == GW_ATTACK_BINARY);
+    if (cfg->force_workgroup && !wg_able) {
+        set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor "
+                "and TeamBattle with BinaryAttackActor");
         return GW_E_UNSUPPORTED;
     }
-    const bool wg = rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE &&
-                    (A > GW_MAX_AGENTS || cfg->force_workgroup);
-    const int max_lanes = wg ? GW_MAX_LANES : GW_MAX_AGENTS;
+    const bool wg = wg_able && (A > GW_MAX_AGENTS || cfg->force_workgroup);
+    const int max_lanes = wg_able ? GW_MAX_LANES : GW_MAX_AGENTS;
     if (A == 0 || A > max_lanes) {
         set_err("%d dynamic entities outside 1..%d (%s)", A, max_lanes,
-                rtt ? "ReachTheTarget: one thread each, SelectiveAttackActor" : "one wavefront lane each");
+                wg_able ? "one workgroup thread each" : "one wavefront lane each");
         return GW_E_UNSUPPORTED;
+    }
+    if (wg && tb) {
+        for (int l = 0; l < A; l++) {
+            const gw_agent_spec& s = cfg->agents[lanes[l]];
+            if ((s.kind & GW_K_ATTACKING) && s.simultaneous_attacks > WG_LIST) {
+                set_err("agent %d: simultaneous_attacks %d > %d on the workgroup kernel", lanes[l],
+                        s.simultaneous_attacks, WG_LIST);
+                return GW_E_UNSUPPORTED;
+            }
+        }
     }
     if ((int)passive.size() > 32 * PAC_MAX_PWORDS) {
         set_err("%d food entities > %d", (int)passive.size(), 32 * PAC_MAX_PWORDS);

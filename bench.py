@@ -438,7 +438,9 @@ def main():
             workload += ' (not the headline metric\'s config)'
         achieved = nbytes / (step_ms_all * 1e-3) / 1e9
         traffic, rocprof_ms = None, None
-        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{"_rollout" if rollout else ""}.json')
+        # the committed rocprofv3 evidence of this exact launch shape (a
+        # rollout profile is per fragment length: tools/profile.sh ... <F>)
+        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{f"_rollout_f{F}" if rollout else ""}.json')
         if args.workload == 'team_battle' and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')

@@ -124,6 +124,17 @@ CASES = [
                     view_range=3)),
     dict(name='maze_16', kind='maze', maze='generate:16:16:2024', n_envs=4, n_steps=200,
          horizon=150, seed_base=9, agent=dict(move_range=1, view_range=2)),
+    # TeamBattle beyond one wavefront: 128 fighters (the engine's workgroup-
+    # per-env kernel), the example's BattleAgent, 2 teams on 24x24
+    dict(name='tb_128', rows=24, cols=24, n_agents=128, n_teams=2, n_envs=2, n_steps=140,
+         horizon=100, seed_base=128),
+    # 100 fighters in 4 teams on 16x16: accuracy < 1, attack range 2, two
+    # stacked attacks, cross-team overlap, observe_self=False
+    dict(name='tb_100', rows=16, cols=16, n_agents=100, n_teams=4, n_envs=2, n_steps=120,
+         horizon=70, seed_base=100, overlap={1: [1, 3], 2: [2], 3: [3], 4: [4, 2]},
+         stacked_attacks=True, observe_self=False,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=0.8,
+                    view_range=2, simultaneous_attacks=2)),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,

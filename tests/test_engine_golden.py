@@ -116,3 +116,18 @@ def test_engine_workgroup_kernel_matches_reference(name):
     r = EngineRunner(g, force_workgroup=True)
     assert r.eng.wg
     replay(r, g)
+
+
+# TeamBattle fixtures with one view range (tb_views mixes them: the one-wave kernel only)
+TB_GOLDEN = [n for n in GOLDEN_CASES if n.startswith('tb') and n != 'tb_views']
+
+
+@pytest.mark.parametrize('name', TB_GOLDEN)
+def test_engine_workgroup_team_battle_matches_reference(name):
+    """The TeamBattle program on the workgroup-per-env kernel (BinaryAttackActor,
+    move isolation, the done components) on every TeamBattle fixture: tb_128
+    and tb_100 take it by size (more than 64 lanes), the others are forced."""
+    g = load_golden(name)
+    r = EngineRunner(g, force_workgroup=True)
+    assert r.eng.wg
+    replay(r, g)

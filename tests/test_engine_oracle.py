@@ -10,13 +10,15 @@ from tests.cases import team_battle, load_golden, build_maze
 pytestmark = pytest.mark.gpu
 
 
-def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1):
+def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1, force_workgroup=False):
     """The oracle holds every entity, the engine one lane per dynamic entity:
     compare the lanes (static entities are constant in both)."""
     import torch
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     seeds = env_seeds(E, run=seed_run)
+    cc.cfg.force_workgroup = int(force_workgroup)
     eng = GridWorldEngine(cc, E, seeds=seeds)
+    assert eng.wg == (force_workgroup or eng.A > 64)
     orc = oracle_mod.Oracle(cc, E)
     orc.seed(seeds)
     NE, ln = cc.n_agents, eng.lane_entities
@@ -82,6 +84,33 @@ def test_dense_attack_configs(oracle_mod, kw):
 def test_dense_configs(oracle_mod, kw):
     cc = team_battle(**kw)
     _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3)
+
+
+@pytest.mark.parametrize('kw', [
+    # 128 BattleAgents on 32x32 (the headline grid with twice the fighters)
+    dict(rows=32, cols=32, n_agents=128, n_teams=2),
+    # 200 fighters, 4 teams, accuracy < 1, stacked double attacks, range 2
+    dict(rows=24, cols=24, n_agents=200, n_teams=4, stacked_attacks=True,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.5, attack_accuracy=0.7,
+                    view_range=3, simultaneous_attacks=2)),
+])
+def test_team_battle_beyond_one_wave(oracle_mod, kw):
+    """TeamBattle with more than 64 fighters: the workgroup-per-env kernel vs
+    the oracle at 1024 envs."""
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=1024, T=120, horizon=60, seed_run=12, key=29, check_every=2)
+
+
+@pytest.mark.parametrize('idx', [0, 3])
+def test_dense_configs_workgroup_kernel(oracle_mod, idx):
+    """Dense TeamBattle configs forced through the workgroup kernel."""
+    kw = [dict(rows=8, cols=8, n_agents=16, n_teams=2),
+          None, None,
+          dict(rows=9, cols=9, n_agents=30, n_teams=2, stacked_attacks=True,
+               agent=dict(move_range=1, attack_range=1, attack_strength=0.4, attack_accuracy=0.9,
+                          view_range=2, simultaneous_attacks=3))][idx]
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, force_workgroup=True)
 
 
 def test_maze_navigation_1024_envs(oracle_mod):

@@ -12,8 +12,8 @@
                                 as roofline.traffic.
 
 usage: python tools/summarize_profile.py <tag> <team_battle|rtt> --mode rollout|step --raw DIR --dest DIR
-(rollout mode: every step-kernel dispatch is a gw_rollout fragment; the
-json is pmc_<kernel>_rollout.json)
+(rollout mode: every step-kernel dispatch is a gw_rollout fragment of
+--fragment steps; the json is pmc_<kernel>_rollout_f<fragment>.json)
 """
 import argparse
 import csv
@@ -60,12 +60,14 @@ def main():
     ap.add_argument('--mode', default='step', choices=['step', 'rollout'])
     ap.add_argument('--stats-args', default='--steps 200 --warmup 20')
     ap.add_argument('--pmc-args', default='--steps 30 --warmup 5')
+    ap.add_argument('--fragment', type=int, default=100)
     a = ap.parse_args()
     kernel = KERNEL[a.workload]
     os.makedirs(a.dest, exist_ok=True)
     sroot = os.path.join(a.raw, f'prof_{a.tag}_stats')
     stats = find(sroot, '*kernel_stats.csv')
-    base = f'{a.tag}_{a.workload}' + ('_rollout' if a.mode == 'rollout' else '')
+    suffix = f'_rollout_f{a.fragment}' if a.mode == 'rollout' else ''
+    base = f'{a.tag}_{a.workload}' + suffix
     shutil.copy(stats, os.path.join(a.dest, base + '_kernel_stats.csv'))
     rows = list(csv.DictReader(open(stats)))
     res = {}
@@ -88,15 +90,15 @@ def main():
            'hbm_bytes_per_launch': 2.0 * fetch + write,
            'hbm_bytes_per_launch_raw': fetch + write,
            'dispatches': {'FETCH_SIZE': nf, 'WRITE_SIZE': nw}, 'avg_ns': avg_ns,
-           'rocprof_avg_ms': avg_ns / 1e6, 'mode': a.mode}
-    suffix = '_rollout' if a.mode == 'rollout' else ''
+           'rocprof_avg_ms': avg_ns / 1e6, 'mode': a.mode,
+           'steps_per_launch': a.fragment if a.mode == 'rollout' else 1}
     json.dump(pmc, open(os.path.join(a.dest, f'pmc_{kernel.split("<")[0]}{suffix}.json'), 'w'), indent=1)
     lines = [f'# rocprofv3 summary `{a.tag}` ({a.workload})', '',
              f'Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py '
-             f'--workload {a.workload} --mode {a.mode} --no-cpu-baseline --no-other --fragment 100 '
+             f'--workload {a.workload} --mode {a.mode} --no-cpu-baseline --no-other --fragment {a.fragment} '
              f'{a.stats_args}`; PMC: `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`, separate runs, '
              f'`{a.pmc_args}` (tools/profile.sh).' +
-             (' Every step-kernel dispatch is a 100-step gw_rollout fragment.' if a.mode == 'rollout' else ''),
+             (f' Every step-kernel dispatch is a {a.fragment}-step gw_rollout fragment.' if a.mode == 'rollout' else ''),
              '',
              '| kernel | calls | avg us | min us | max us | % |', '|---|---|---|---|---|---|']
     for r in rows:
