@@ -93,6 +93,7 @@ struct Params {
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
     int32_t pair_cap;                      // crowded (observer, cell) pairs that fit after the obs stage
+    int32_t nact_off;                      // parked next-step actions: offset in the work area
     int32_t act_dim;                       // ints per entity action (gw_config_act_dim)
     int32_t attack_kind;                   // GW_ATTACK_*
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
@@ -197,6 +198,17 @@ __device__ __forceinline__ double rld(double v, int l)
 
 __device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
 
+// s_setprio with a wave-uniform level (0..3; the instruction takes an immediate)
+__device__ __forceinline__ void set_prio(int v)
+{
+    switch (v) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 // ------------------------------------------------------------ checked build
 // -DGW_CHECKS: every data-dependent LDS index and every "exactly one lane"
 // ballot is validated; a violation is recorded in p.dbg and the access is
@@ -275,8 +287,27 @@ __device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
         if (lane_id() == 0 && p.stamps) p.stamps[(size_t)e * GW_STAMP_STRIDE + (i)] = _t;      \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
+// launch-level placement of the wave: [60] s_memrealtime at the start, [61]
+// at the end (100 MHz, one clock for the whole device), [62] HW_ID (CU, SIMD,
+// SE), [63] XCC_ID (tools/tail_probe.py)
+#define STAMP_WAVE(slot, with_ids)                                                \
+    do {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        uint64_t _t = __builtin_amdgcn_s_memrealtime();                           \
+        if (lane_id() == 0 && p.stamps) {                                         \
+            p.stamps[(size_t)e * GW_STAMP_STRIDE + (slot)] = _t;                  \
+            if (with_ids) {                                                       \
+                p.stamps[(size_t)e * GW_STAMP_STRIDE + 62] =                      \
+                    (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);          \
+                p.stamps[(size_t)e * GW_STAMP_STRIDE + 63] =                      \
+                    (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);         \
+            }                                                                     \
+        }                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+    } while (0)
 #else
 #define STAMP(i) do { } while (0)
+#define STAMP_WAVE(slot, with_ids) do { } while (0)
 #endif
 
 // ------------------------------------------------------------ MT19937
@@ -472,6 +503,7 @@ struct Smem {
     uint32_t* tcnt;
     uint32_t* scnt;
     int8_t* stage;
+    int32_t* nact;          // step kernel: the next step's actions [64][3] (gw_rollout)
 };
 
 // Jacobi placement scratch in the work area (do_reset): stream words,
@@ -490,10 +522,15 @@ constexpr size_t JAC_WORK_BYTES = JAC_OFF_KEY2 + 4 * GW_MT_N;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// the step kernel's parked next-step actions [64][3] (gw_rollout) sit at the
+// end of the work area: after the observation stage and its crowded-pair
+// list, clobbered by a reset's placement (the kernel then re-reads them)
+constexpr size_t NACT_BYTES = WAVE * 3 * 4;
+
 __host__ __device__ inline size_t work_bytes(int HW, int A, int S, int max_enc)
 {
     size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
-    size_t s = align16((size_t)A * S * ((S + 3) & ~3));     // observation stage [A][S][SP]
+    size_t s = align16((size_t)A * S * ((S + 3) & ~3)) + NACT_BYTES;     // observation stage [A][S][SP]
     (void)max_enc;
     if (s < w) s = w;
     return s > JAC_WORK_BYTES ? s : JAC_WORK_BYTES;
@@ -515,6 +552,7 @@ __device__ __forceinline__ Smem carve(char* base, const Params& p)
     s.tcnt = (uint32_t*)base;
     s.scnt = (uint32_t*)(base + align16((size_t)((HW + 3) / 4) * 4));
     s.stage = (int8_t*)base;
+    s.nact = (int32_t*)(base + p.nact_off);
     return s;
 }
 
@@ -720,10 +758,13 @@ __device__ __forceinline__ void compact_stage(Smem& sm, int A)
 }
 
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
-template <int S>
+template <int S, bool PLAIN = false>
 __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
                                             int32_t* obs, int stamp_base = 8)
 {
+    // PLAIN (step_kernel<S, 1>): no blocking entities, one view range, every observer
+    const bool HV = !PLAIN && p.hetero_view, BL = !PLAIN && p.blockers, LB = !PLAIN && p.lane_blockers;
+    const int OO = PLAIN ? -1 : p.obs_only;
     (void)stamp_base;
     constexpr int SS = S * S;
     constexpr int R = S / 2;
@@ -733,8 +774,8 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     constexpr int SSP = S * SP;
     const int l = lane_id();
     const int A = p.A;
-    // (gw_component OBSERVE: the one lane p.obs_only, whatever its done state)
-    const bool obs_me = (p.obs_only >= 0 ? l == p.obs_only : (l < A && L.live)) &&
+    // (gw_component OBSERVE: the one lane OO, whatever its done state)
+    const bool obs_me = (OO >= 0 ? l == OO : (l < A && L.live)) &&
                         (L.kind & GW_K_GRID_OBSERVER);
     // persistent obs buffer (gw_config.persistent_obs): rows that already
     // hold -2 and stay -2 (done entities, non-observers) are not rewritten
@@ -743,11 +784,11 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me)
                         : (p.skip_done_obs ? __ballot(l < A && !obs_me) : 0ull);
     if (l < A) L.obs_m2 = p.persistent_obs && !obs_me;
-    // observers with different view ranges (p.hetero_view): lane l's window
+    // observers with different view ranges (HV): lane l's window
     // of range vw <= R sits in the top-left (2vw+1)^2 of its S x S slot, the
     // rest of the slot is -2 (the reference's per-agent (2v+1)^2 obs,
     // observer.py:162-174, in one tensor shape)
-    const int vw = p.hetero_view ? (obs_me ? L.view : 0) : R;
+    const int vw = HV ? (obs_me ? L.view : 0) : R;
 
     // cells hidden by blocking entities (create_grid_and_mask, utils.py:46-115):
     // static blockers precomputed per cell, blocking lanes from the shadow LUT
@@ -755,14 +796,14 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     uint32_t hid[MW];
 #pragma unroll
     for (int w = 0; w < MW; w++) hid[w] = 0u;
-    if (p.blockers && p.hetero_view) {
+    if (BL && HV) {
         // slot-geometry LUTs per range (bit wr * S + wc)
         if (obs_me && p.hsmask_off[vw] >= 0) {
             const uint32_t* src = p.hsmask + p.hsmask_off[vw] + (size_t)(L.r * p.W + L.c) * MW;
 #pragma unroll
             for (int w = 0; w < MW; w++) hid[w] = src[w];
         }
-        if (p.lane_blockers) {
+        if (LB) {
             for (uint64_t bl = __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
                 const int b = first_lane(bl);
                 const int dr = rl(L.r, b) - L.r, dc = rl(L.c, b) - L.c;
@@ -774,13 +815,13 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                 }
             }
         }
-    } else if (p.blockers) {
+    } else if (BL) {
         if (obs_me && p.smask_off[R] >= 0) {
             const uint32_t* src = p.smask + p.smask_off[R] + (size_t)(L.r * p.W + L.c) * MW;
 #pragma unroll
             for (int w = 0; w < MW; w++) hid[w] = src[w];
         }
-        if (p.lane_blockers) {
+        if (LB) {
             for (uint64_t bl = __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
                 const int b = first_lane(bl);
                 const int dr = rl(L.r, b) - L.r, dc = rl(L.c, b) - L.c;
@@ -854,10 +895,10 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         if (obs_me) {
             using T = std::integral_constant<bool, true>;
             using F = std::integral_constant<bool, false>;
-            if (p.hetero_view) {
-                if (p.blockers) stage_rows(T(), T());
+            if (HV) {
+                if (BL) stage_rows(T(), T());
                 else stage_rows(F(), T());
-            } else if (p.blockers) {
+            } else if (BL) {
                 stage_rows(T(), F());
             } else {
                 stage_rows(F(), F());
@@ -928,7 +969,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             const int orr = __shfl(L.r, o), occ = __shfl(L.c, o);
             const uint32_t oseq = __shfl(L.seq, o);
             const bool o_in = __shfl((int)L.in_grid, o) != 0;
-            const int ov = p.hetero_view ? __shfl(vw, o) : R;     // the observer's window origin
+            const int ov = HV ? __shfl(vw, o) : R;     // the observer's window origin
             const int gr = orr - ov + pwr, gc = occ - ov + pwc;
             const int gcell = gr * p.W + gc;
             const bool self_in = !p.observe_self && o_in && orr == gr && occ == gc;
@@ -987,7 +1028,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         const int o = first_lane(olanes);
         olanes &= olanes - 1;
         const int orr = rl(L.r, o), oc = rl(L.c, o);
-        const int ov = p.hetero_view ? rl(vw, o) : R;
+        const int ov = HV ? rl(vw, o) : R;
         for (int k0 = 0; k0 < SS; k0 += WAVE) {
             const int k = k0 + l;
             const int sidx = o * SSP + (k / S) * SP + k % S;
@@ -1103,9 +1144,11 @@ __device__ __forceinline__ bool attack_precheck(const Params& p, const Smem& sm,
 // BinaryAttackActor.process_action for attacker a with k attacks.
 // Returns status (attempted); list (register of lane t) = attacked lanes in
 // list order; applies damage and updates the cell table for kills.
+template <bool PLAIN = false>
 __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, Lane& L, int a,
                                            int k, int& nlist, int& list)
 {
+    const bool BL = !PLAIN && p.blockers, LB = !PLAIN && p.lane_blockers;
     const int l = lane_id();
     nlist = 0;
     list = -1;
@@ -1120,12 +1163,12 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
     const int dr = L.r - ar, dc = L.c - ac;
     bool cand = l < p.A && L.in_grid && l != a && L.active && ((amap >> L.enc) & 1u) &&
                 dr >= -R && dr <= R && dc >= -R && dc <= R;
-    if (p.blockers) {                                       // attack mask (actor.py:483-494)
+    if (BL) {                                       // attack mask (actor.py:483-494)
         const int k = (dr + R) * D + (dc + R), mw = mask_words(R);
         bool hidden = false;
         if (cand && p.smask_off[R] >= 0)
             hidden = (p.smask[p.smask_off[R] + (size_t)(ar * p.W + ac) * mw + (k >> 5)] >> (k & 31)) & 1u;
-        if (p.lane_blockers) {
+        if (LB) {
             for (uint64_t bl = __ballot(l < p.A && L.active && (L.kind & GW_K_BLOCKING)); bl; bl &= bl - 1) {
                 const int b = first_lane(bl);
                 const int bdr = rl(L.r, b) - ar, bdc = rl(L.c, b) - ac;
@@ -1897,7 +1940,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     return ok;
 }
 
-template <int S>
+template <int S, bool PLAIN = false>
 __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr,
                                           bool fused, int32_t* obs)
 {
@@ -1916,7 +1959,7 @@ __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng&
             wave_sync();
         }
         build_tables(p, sm, L, !fused);
-        observe_all<S>(p, e, sm, rng, L, obs, 26);
+        observe_all<S, PLAIN>(p, e, sm, rng, L, obs, 26);
     } else {
         int32_t* out = obs + (size_t)e * p.A * SS;
         for (int i = lane_id(); i < p.A * SS; i += WAVE) out[i] = -2;
@@ -1952,9 +1995,24 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_STEP_WAVES_PER_EU
 #define GW_STEP_WAVES_PER_EU 4
 #endif
-template <int S>
+#ifndef GW_PROGRESS_PRIO
+#define GW_PROGRESS_PRIO 1
+#endif
+#ifndef GW_PREFETCH_ACTIONS
+#define GW_PREFETCH_ACTIONS 1
+#endif
+#ifndef GW_STEP_SPEC
+#define GW_STEP_SPEC 1
+#endif
+// SPEC 1: the TeamBattle program without blocking entities and with one
+// view range (BASELINE's headline config): the other programs' passes and
+// the masked / mixed-range observation fold away at compile time (the
+// generic kernel holds every program, and its register pressure spills)
+template <int S, int SPEC = 0>
 __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params p)
 {
+    constexpr bool PLAIN = SPEC == 1;
+    const int sim_kind = PLAIN ? (int)GW_SIM_TEAM_BATTLE : p.sim_kind;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int e = blockIdx.x;
     if (e >= p.E) return;
@@ -1963,6 +2021,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     const bool valid = l < A;
     constexpr int SS = S * S;
     STAMP(0);
+    STAMP_WAVE(60, true);
     Smem sm = carve(smem_raw, p);
     // every global load of the prologue is issued before any is used (one
     // memory round trip): the epilogue counters, the previous __all__ (read
@@ -1990,17 +2049,46 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     // the LDS table holds the template (load_env); lanes are added before
     // the first step that needs them (a reset adds its own)
     bool lanes_in = false, need_tmpl = false;
+    int pa0 = 0, pa1 = 0, pa2 = 0;             // actions of step t + 1 (prefetched)
+    bool nact_ok = false;                       // sm.nact holds them
     for (int t = 0; t < p.nsteps; t++) {
+        // progress priority (gw_rollout): the four envs of a SIMD start
+        // together, and VALU issue goes by priority, then age, so the youngest
+        // wave would trail the others and end the launch alone; a wave drops
+        // one level per quarter of the fragment it has done, so the SIMD's
+        // waves stay within about a quarter of each other
+        int prio = 0;
+        if (GW_PROGRESS_PRIO && p.nsteps > 1) prio = 3 - min(3, (4 * t) / p.nsteps);
+        set_prio(prio);
+        STAMP(50);
         const int32_t* act_t = p.actions + (size_t)t * EA * p.act_dim;
         int32_t* obs_t = p.obs + (size_t)t * EA * SS;
         double* rew_t = p.reward + (size_t)t * EA;
         uint8_t* done_t = p.done + (size_t)t * EA;
         uint8_t* ad_t = p.all_done + (size_t)t * p.E;
-        if (t > 0) {
+        // the next step's actions are loaded at the top of this step, before
+        // this step's stores (vmcnt counts loads and stores in issue order: a
+        // load issued at the top of step t+1 would wait for step t's stores as
+        // well), and parked in LDS (sm.nact) once the step's first passes are
+        // done, so that they hold no registers through the observation
+        if (t > 0 && (!GW_PREFETCH_ACTIONS || !nact_ok)) {
             const int32_t* ap = act_t + act_row;
             const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
             mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
+        } else if (t > 0) {
+            const int32_t* na = sm.nact + 3 * l;
+            const int a0 = na[0], a1 = na[1], a2 = na[2];
+            mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
         }
+        const bool prefetch = GW_PREFETCH_ACTIONS && t + 1 < p.nsteps;
+        if (prefetch) {
+            const int32_t* ap = act_t + (size_t)EA * p.act_dim + act_row;
+            pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
+        }
+        nact_ok = false;
+        auto park = [&]() {
+            if (prefetch) { int32_t* na = sm.nact + 3 * l; na[0] = pa0; na[1] = pa1; na[2] = pa2; nact_ok = true; }
+        };
         if (need_tmpl) { table_template(p, sm); lanes_in = false; need_tmpl = false; }
         // NEXT_STEP auto-reset: the episode ended in the previous step, so this
         // step is AllStepManager.reset for the env (actions ignored): obs =
@@ -2017,7 +2105,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             L.reward = 0.0;
             bool raised = false;                 // ReachTheTarget's double remove (KeyError)
 
-            if (p.sim_kind == GW_SIM_TEAM_BATTLE) {
+            if (sim_kind == GW_SIM_TEAM_BATTLE) {
                 // ---- attack pass (team_battle_example.py:35-47)
                 const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
                 const bool maybe = att && L.active && attack_precheck(p, sm, L);
@@ -2026,8 +2114,8 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // serial attack chain gets issue priority over the SIMD's other waves
                 {
                     const int nser = __popcll(maybe_mask);
-                    if (nser >= 16) __builtin_amdgcn_s_setprio(2);
-                    else if (nser >= 8) __builtin_amdgcn_s_setprio(1);
+                    if (nser >= 16 && prio < 2) set_prio(2);
+                    else if (nser >= 8 && prio < 1) set_prio(1);
         #ifdef GW_STAMPS
                     const int natt = __popcll(__ballot(att));
                     if (l == 0 && p.stamps) {
@@ -2051,7 +2139,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     }
                     if (!rlb(L.active, a)) continue;                // killed earlier this pass
                     int nlist, list;
-                    attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                    attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
                         for (int t = 0; t < nlist; t++) {
@@ -2120,7 +2208,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 wave_sync();
                 if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
                 wave_sync();
-            } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+            } else if (sim_kind == GW_SIM_REACH_TARGET) {
                 // ---- attack pass (reach_the_target.py:96-108): every acting agent,
                 // dict order; only AttackingAgents attack (others return False, [])
                 const int32_t* act_e = act_t + (size_t)e * A * p.act_dim;
@@ -2130,7 +2218,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     int nlist, list;
                     const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
                         ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
-                        : attack_one(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                        : attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
                     if (!status) continue;
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
@@ -2179,7 +2267,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     // the LDS table after the passes (observation)
                     build_tables(p, sm, L, true);
                 }
-            } else if (p.sim_kind == GW_SIM_TRAFFIC) {
+            } else if (sim_kind == GW_SIM_TRAFFIC) {
                 // ---- traffic_corridor.py:41-49: the action dict in dict order;
                 // a failed move (None for non-MovingAgents) -0.1, then +1 when
                 // get_done(agent) holds right after the agent's own move
@@ -2191,7 +2279,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 }
                 ctr += (uint32_t)WAVE;
                 build_tables(p, sm, L, true);       // the LDS table after the moves
-            } else if (p.sim_kind == GW_SIM_MAZE_NAV) {
+            } else if (sim_kind == GW_SIM_MAZE_NAV) {
                 const int n = p.nav, t = p.target;
                 if ((act_mask >> n) & 1) {
                     const int pr = rl(L.r, n), pc = rl(L.c, n);
@@ -2214,6 +2302,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 }
             }
             STAMP(3);
+            park();
             if (raised) {
                 // Grid.remove raised KeyError: the step stops here (no further
                 // moves, no observation draws, its outputs are not written); the
@@ -2231,16 +2320,16 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
 
                 // ---- observations of the live agents (all_step_manager.py:68-71)
                 STAMP(4);
-                observe_all<S>(p, e, sm, rng, L, obs_t);
+                observe_all<S, PLAIN>(p, e, sm, rng, L, obs_t);
                 STAMP(5);
 
                 // ---- rewards, dones (:72-79, smart.py:101-111)
                 bool dn;
                 bool only_left = false;                 // OnlyAgentLeftDone (reach_the_target.py:41-55)
-                if (p.sim_kind == GW_SIM_MAZE_NAV) {
+                if (sim_kind == GW_SIM_MAZE_NAV) {
                     const int n = p.nav, t = p.target;
                     dn = rl(L.r, n) == rl(L.r, t) && rl(L.c, n) == rl(L.c, t);
-                } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+                } else if (sim_kind == GW_SIM_REACH_TARGET) {
                     const int t = p.target;
                     const bool is_agent = (L.kind & GW_K_OBSERVING) && (L.kind & GW_K_ACTING);
                     only_left = __popcll(__ballot(valid && is_agent && L.active)) <= 1;
@@ -2258,9 +2347,9 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 const bool live_after = valid && L.live && !dn;
                 // get_all_done (done.py:49-56,147-153) or maze target reached
                 bool all;
-                if (p.sim_kind == GW_SIM_MAZE_NAV) {
+                if (sim_kind == GW_SIM_MAZE_NAV) {
                     all = dn;
-                } else if (p.sim_kind == GW_SIM_REACH_TARGET) {
+                } else if (sim_kind == GW_SIM_REACH_TARGET) {
                     all = only_left;
                 } else {
                     all = true;
@@ -2285,12 +2374,15 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             }
         }
         if (reset_now) {
+            // (the placement's scratch overlaps the parked actions: the next
+            // step re-reads its actions from memory)
+            nact_ok = false;
             // the reset is the launch's critical path: issue it ahead of the
             // SIMD's stepping waves
             __builtin_amdgcn_s_setprio(3);
             wave_sync();
             STAMP(12);
-            reset_env<S>(p, e, sm, rng, L, ctr, true, obs_t);
+            reset_env<S, PLAIN>(p, e, sm, rng, L, ctr, true, obs_t);
             STAMP(14);
             steps = 0;
             lanes_in = true;
@@ -2303,7 +2395,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 if (l == 0) ad_t[e] = 0;
                 prev_all = false;
             }
-            __builtin_amdgcn_s_setprio(0);
+            set_prio(prio);
         }
     }
     if (l == 0) {
@@ -2313,6 +2405,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
     STAMP(6);
+    STAMP_WAVE(61, false);
 }
 
 // The component plugin API (state.py / actor.py / observer.py), one
@@ -2532,7 +2625,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 // in their own translation unit (-DGW_PART_S=<S>; _native.build compiles the
 // parts in parallel and links them with the host part).  Each part exports a
 // launcher and an attribute setter; the host part dispatches on S to them.
-enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4 };
+enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5 };
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
@@ -2552,7 +2645,8 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     const Params& p = *static_cast<const Params*>(params);
     constexpr int S = GW_PART_S;
     switch (kind) {
-    case PK_STEP: hipLaunchKernelGGL(step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP: hipLaunchKernelGGL((step_kernel<S, 0>), dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP_TB: hipLaunchKernelGGL((step_kernel<S, 1>), dim3(grid), dim3(block), smem, st, p); break;
     case PK_RESET: hipLaunchKernelGGL(reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_STEP: hipLaunchKernelGGL(wg_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
@@ -2565,7 +2659,8 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
 hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
 {
     constexpr int S = GW_PART_S;
-    const void* k = kind == PK_STEP ? (const void*)step_kernel<S>
+    const void* k = kind == PK_STEP ? (const void*)step_kernel<S, 0>
+                  : kind == PK_STEP_TB ? (const void*)step_kernel<S, 1>
                   : kind == PK_RESET ? (const void*)reset_kernel<S>
                   : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
                   : kind == PK_COMP ? (const void*)comp_kernel<S>
@@ -2589,6 +2684,7 @@ struct gw_engine {
     uint32_t* d_hsmask;
     int32_t lane_ent[GW_MAX_LANES];
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
+    bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
     PolicySpec policy;
     size_t smem_step, smem_reset;
     // Pacman program
@@ -2686,7 +2782,7 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
-    return part_launch(g, g->wg ? PK_WG_STEP : PK_STEP, g->smem_step, p, st);
+    return part_launch(g, g->wg ? PK_WG_STEP : (g->step_tb ? PK_STEP_TB : PK_STEP), g->smem_step, p, st);
 }
 
 static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
@@ -3097,7 +3193,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             p.hsmask = g->d_hsmask;
         }
     }
-    p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
+    p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - NACT_BYTES -
+                        (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
+    p.nact_off = (int32_t)(work_bytes(HW, A, g->S, max_enc) - NACT_BYTES);
     g->smem_step = smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
         const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE;
@@ -3175,6 +3273,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     if (wg) HIPCHK(set_part_attrs(g->S, PK_WG_STEP, PK_WG_RESET, g->smem_step, g->smem_step));
     else if (!pac) HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
+    g->step_tb = GW_STEP_SPEC && !wg && !pac && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
+                 !p.hetero_view;
+    if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));
     *out = g;
     return GW_OK;
 }

@@ -17,6 +17,7 @@ CHILD = r'''
 import ctypes as C, json, sys, time
 sys.path.insert(0, %(root)r)
 import numpy as np, torch
+REPS = int(%(reps)r)
 from abmarl_amd import _native
 _native.LIB = %(lib)r
 sigs = dict(_native.SIGNATURES)
@@ -52,25 +53,26 @@ if hasattr(L, 'gw_rollout'):
     for F in (20, 100):
         acts = torch.empty((F,) + tuple(eng.actions.shape), dtype=torch.int32, device=eng.device)
         out = eng.rollout_buffers(F)
-        for skip in (False, True):
-            best = None
-            for rep in range(3):
-                for s in range(F):
-                    eng.random_actions(9, 100000 + rep * F + s, out=acts[s])
-                torch.cuda.synchronize()
-                a0 = int(eng.acting.sum().item())
-                t0 = time.perf_counter()
-                eng.rollout(acts, horizon=H, skip_done_obs=skip, out=out)
-                torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-                r = ((int(eng.acting.sum().item()) - a0) / dt, dt / F * 1e3)
-                best = r if best is None or r[0] > best[0] else best
-            res[f'rollout{F}{"_skip" if skip else ""}'] = {'agent_steps_per_s': best[0], 'ms_per_step': best[1]}
+        rates = []
+        for rep in range(REPS):
+            for s in range(F):
+                eng.random_actions(9, 100000 + rep * F + s, out=acts[s])
+            torch.cuda.synchronize()
+            a0 = int(eng.acting.sum().item())
+            t0 = time.perf_counter()
+            eng.rollout(acts, horizon=H, skip_done_obs=True, out=out)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            rates.append(((int(eng.acting.sum().item()) - a0) / dt, dt / F * 1e3))
+        rates.sort()
+        res[f'rollout{F}_skip'] = {'agent_steps_per_s_median': rates[len(rates) // 2][0],
+                                   'ms_per_step_median': sorted(r[1] for r in rates)[len(rates) // 2],
+                                   'agent_steps_per_s_best': rates[-1][0]}
 print(json.dumps(res))
 '''
 
 for lib in sys.argv[1:]:
-    out = subprocess.run([sys.executable, '-c', CHILD % dict(root=ROOT, lib=os.path.abspath(lib))],
+    out = subprocess.run([sys.executable, '-c', CHILD % dict(root=ROOT, lib=os.path.abspath(lib), reps=os.environ.get('AB_REPS', '7'))],
                          capture_output=True, text=True, timeout=300)
     line = [x for x in out.stdout.splitlines() if x.startswith('{')]
     print(line[-1] if line else json.dumps({'lib': lib, 'error': out.stderr[-800:]}), flush=True)
