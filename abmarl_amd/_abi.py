@@ -7,7 +7,7 @@ import ctypes as C
 
 GW_MAX_AGENTS = 64
 GW_MAX_LANES = 256
-GW_KERNEL_WAVE, GW_KERNEL_WORKGROUP, GW_KERNEL_PACMAN = 0, 1, 2
+GW_KERNEL_WAVE, GW_KERNEL_WORKGROUP, GW_KERNEL_PACMAN, GW_KERNEL_LANE = 0, 1, 2, 3
 GW_MAX_ENTITIES = 4096
 GW_MAX_ENC = 15
 GW_MAX_CELLS = 4096
@@ -123,6 +123,7 @@ class Config(C.Structure):
         ("force_workgroup", C.c_int32),
         ("persistent_obs", C.c_int32),
         ("all_lanes", C.c_int32),
+        ("env_per_lane", C.c_int32),
     ]
 
 

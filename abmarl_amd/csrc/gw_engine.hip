@@ -2617,6 +2617,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 #include "gw_pacman.inc"
 #endif
 #include "gw_rtt.inc"
+#include "gw_lane.inc"
 
 }  // namespace
 
@@ -2625,7 +2626,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 // in their own translation unit (-DGW_PART_S=<S>; _native.build compiles the
 // parts in parallel and links them with the host part).  Each part exports a
 // launcher and an attribute setter; the host part dispatches on S to them.
-enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5 };
+enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5, PK_STEP_LANE = 6 };
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
@@ -2651,6 +2652,7 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     case PK_WG_STEP: hipLaunchKernelGGL(wg_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_COMP: hipLaunchKernelGGL(comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP_LANE: hipLaunchKernelGGL(lane_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2664,6 +2666,7 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
                   : kind == PK_RESET ? (const void*)reset_kernel<S>
                   : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
                   : kind == PK_COMP ? (const void*)comp_kernel<S>
+                  : kind == PK_STEP_LANE ? (const void*)lane_step_kernel<S>
                                        : (const void*)wg_reset_kernel<S>;
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
@@ -2685,6 +2688,8 @@ struct gw_engine {
     int32_t lane_ent[GW_MAX_LANES];
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
+    bool lane_envs;            // lane_step_kernel<S>: MazeNavigation, one lane per env (gw_lane.inc)
+    size_t smem_lane;          // its dynamic LDS: the per-config tables
     PolicySpec policy;
     size_t smem_step, smem_reset;
     // Pacman program
@@ -2763,7 +2768,8 @@ static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const P
 {
     if (g->S < 1 || g->S > 15 || !(g->S & 1)) return hipErrorInvalidValue;
     const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET) ? WAVE * p.nwv : WAVE;
-    return k_part_launch[g->S >> 1](kind, (unsigned)g->E, block, smem, st, &p);
+    const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + WAVE - 1) / WAVE) : (unsigned)g->E;
+    return k_part_launch[g->S >> 1](kind, grid, block, smem, st, &p);
 }
 
 static hipError_t set_part_attrs(int S, int k0, int k1, size_t a, size_t b)
@@ -2782,6 +2788,7 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
+    if (g->lane_envs) return part_launch(g, PK_STEP_LANE, g->smem_lane, p, st);
     return part_launch(g, g->wg ? PK_WG_STEP : (g->step_tb ? PK_STEP_TB : PK_STEP), g->smem_step, p, st);
 }
 
@@ -3276,6 +3283,36 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     g->step_tb = GW_STEP_SPEC && !wg && !pac && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
                  !p.hetero_view;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));
+    // MazeNavigation with the navigator and the target as its only lanes
+    // (walls static), both at initial positions that never fail to place, no
+    // health, no blocking lane, the target a plain entity: one lane per env
+    // (gw_lane.inc)
+    {
+        bool able = maze && A == 2 && !pac && !wg && !p.lane_blockers && !p.hetero_view && p.nav >= 0 &&
+                    p.target >= 0 && p.nav != p.target;
+        for (int l = 0; able && l < A; l++) {
+            if (hs[l].init_r < 0 || hs[l].init_c < 0 || (hs[l].kind & GW_K_HEALTH)) able = false;
+            if (l == p.target && (hs[l].kind & dynamic_kinds)) able = false;
+        }
+        if (able && hs[0].init_r == hs[1].init_r && hs[0].init_c == hs[1].init_c &&
+            !((hs[1].ov >> hs[0].enc) & 1u))
+            able = false;                                   // the reset's Grid.place would fail
+        // its LDS: padded template + static-blocker masks at the view range +
+        // static-cell bits (lane_step_kernel's carve-up)
+        const int S = g->S, R = S / 2, MWS = (S * S + 31) / 32;
+        const size_t nsm = (p.blockers && p.smask_off[R] >= 0) ? (size_t)HW * MWS : 0;
+        g->smem_lane = 16 * (size_t)((p.tbl_rows * p.pitch + 15) / 16) + 4 * ((nsm + 3) & ~(size_t)3) +
+                       (p.static_bits ? 4 * (size_t)((HW + 31) / 32) : 0);
+        const size_t static_lds = (size_t)WAVE * 2 * S * S + 4 * GW_MT_N;
+        if (g->smem_lane + static_lds > 64 * 1024) able = false;
+        if (cfg->env_per_lane > 0 && !able) {
+            set_err("env_per_lane: the one-lane-per-env kernel runs MazeNavigation with the navigator and "
+                    "the target at initial positions as its only dynamic entities");
+            return GW_E_UNSUPPORTED;
+        }
+        g->lane_envs = able && cfg->env_per_lane >= 0;
+        if (g->lane_envs) HIPCHK(set_part_attrs(g->S, PK_STEP_LANE, PK_STEP_LANE, g->smem_lane, g->smem_lane));
+    }
     *out = g;
     return GW_OK;
 }
@@ -3299,7 +3336,8 @@ int32_t gw_obs_side(gw_handle g) { return g ? g->S : 0; }
 int32_t gw_num_lanes(gw_handle g) { return g ? g->A : 0; }
 int32_t gw_env_kernel(gw_handle g)
 {
-    return !g ? -1 : g->pacman ? GW_KERNEL_PACMAN : g->wg ? GW_KERNEL_WORKGROUP : GW_KERNEL_WAVE;
+    return !g ? -1 : g->pacman ? GW_KERNEL_PACMAN : g->wg ? GW_KERNEL_WORKGROUP
+                   : g->lane_envs ? GW_KERNEL_LANE : GW_KERNEL_WAVE;
 }
 int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
 

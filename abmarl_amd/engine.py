@@ -52,7 +52,9 @@ class GridWorldEngine:
         # die, overlap nothing) live in the engine's cell template
         self.A = int(self.L.gw_num_lanes(h))
         # ReachTheTarget beyond 64 lanes runs on a workgroup per env (gw_rtt.inc)
-        self.wg = int(self.L.gw_env_kernel(h)) == _abi.GW_KERNEL_WORKGROUP
+        # GW_KERNEL_*: MazeNavigation runs one env per lane (gw_lane.inc)
+        self.kernel = int(self.L.gw_env_kernel(h))
+        self.wg = self.kernel == _abi.GW_KERNEL_WORKGROUP
         ents = (C.c_int32 * self.A)()
         _native.check(self.L.gw_lane_entities(h, ents), 'gw_lane_entities')
         self.lane_entities = np.array(ents[:], dtype=np.int64)

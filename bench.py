@@ -202,9 +202,9 @@ def quick_config(name, steps=200, warmup=400):
 
 WORKLOADS = {
     # name: (builder, default envs per GPU, step-kernel name, description)
-    'team_battle': (team_battle_sim, 4096, 'step_kernel<7>',
+    'team_battle': (team_battle_sim, 4096, 'step_kernel<7, 1>',
                     'TeamBattle 32x32, 64 agents / 2 teams'),
-    'maze': (maze_sim, 1024, 'step_kernel<5>',
+    'maze': (maze_sim, 1024, 'lane_step_kernel<5>',
              'MazeNavigation 16x16 (BASELINE config 2), 1 navigator, blocking walls'),
     'rtt': (rtt_sim, 1024, 'wg_step_kernel<7>',
             'ReachTheTarget 64x64 (BASELINE config 4), 256 entities'),
@@ -441,7 +441,7 @@ def main():
         # the committed rocprofv3 evidence of this exact launch shape (a
         # rollout profile is per fragment length: tools/profile.sh ... <F>)
         pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{f"_rollout_f{F}" if rollout else ""}.json')
-        if args.workload == 'team_battle' and os.path.exists(pmc):
+        if args.workload in ('team_battle', 'maze') and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')
             rocprof_ms = prof.get('rocprof_avg_ms')

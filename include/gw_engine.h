@@ -209,6 +209,12 @@ typedef struct gw_config {
     /* 1: every entity is a lane (no static entities in the cell template):
        the component plugin API keeps all entity state in lanes              */
     int32_t  all_lanes;
+    /* one-lane-per-env kernel (MazeNavigation with the navigator and the
+       target as its only dynamic entities, both at initial positions: 64
+       envs per wave): 0 = automatic (used when eligible), 1 = required
+       (gw_create fails if the config is not eligible), -1 = never (one
+       wavefront per env)                                                     */
+    int32_t  env_per_lane;
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack
@@ -436,10 +442,12 @@ int32_t     gw_num_passive(gw_handle h);
 int32_t     gw_num_lanes(gw_handle h);
 /* the step kernel's execution model: GW_KERNEL_WAVE (one wavefront per env),
    GW_KERNEL_WORKGROUP (ReachTheTarget: one workgroup of ceil(A/64) waves per
-   env), GW_KERNEL_PACMAN (the Pacman program, one wavefront per env)         */
+   env), GW_KERNEL_PACMAN (the Pacman program, one wavefront per env),
+   GW_KERNEL_LANE (MazeNavigation: one lane per env, 64 envs per wave)       */
 #define GW_KERNEL_WAVE      0
 #define GW_KERNEL_WORKGROUP 1
 #define GW_KERNEL_PACMAN    2
+#define GW_KERNEL_LANE      3
 int32_t     gw_env_kernel(gw_handle h);
 int32_t     gw_act_dim(gw_handle h);
 /* entity index (into gw_config.agents) of each lane; out: host int32[A]     */

@@ -10,15 +10,19 @@ from tests.cases import team_battle, load_golden, build_maze
 pytestmark = pytest.mark.gpu
 
 
-def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1, force_workgroup=False):
+def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1, force_workgroup=False,
+         env_per_lane=0, kernel=None):
     """The oracle holds every entity, the engine one lane per dynamic entity:
     compare the lanes (static entities are constant in both)."""
     import torch
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     seeds = env_seeds(E, run=seed_run)
     cc.cfg.force_workgroup = int(force_workgroup)
+    cc.cfg.env_per_lane = int(env_per_lane)
     eng = GridWorldEngine(cc, E, seeds=seeds)
     assert eng.wg == (force_workgroup or eng.A > 64)
+    if kernel is not None:
+        assert eng.kernel == kernel, (eng.kernel, kernel)
     orc = oracle_mod.Oracle(cc, E)
     orc.seed(seeds)
     NE, ln = cc.n_agents, eng.lane_entities
@@ -113,11 +117,17 @@ def test_dense_configs_workgroup_kernel(oracle_mod, idx):
     _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, force_workgroup=True)
 
 
-def test_maze_navigation_1024_envs(oracle_mod):
+@pytest.mark.parametrize('kernel', ['lane', 'wave'])
+def test_maze_navigation_1024_envs(oracle_mod, kernel):
     """BASELINE config 2: MazeNavigation 16x16 (generate_maze walls, blocking),
-    1 navigator, 1024 envs, random moves, horizon auto-reset."""
+    1 navigator, 1024 envs, random moves, horizon auto-reset; on the
+    one-lane-per-env kernel (the default for this config) and the one-wave
+    kernel."""
+    from abmarl_amd import _abi
     cc = build_maze(load_golden('maze_16')['case']).compiled()
-    _run(oracle_mod, cc, E=1024, T=300, horizon=120, seed_run=2, key=5)
+    _run(oracle_mod, cc, E=1024, T=300, horizon=120, seed_run=2, key=5,
+         env_per_lane=0 if kernel == 'lane' else -1,
+         kernel=_abi.GW_KERNEL_LANE if kernel == 'lane' else _abi.GW_KERNEL_WAVE)
 
 
 @pytest.mark.parametrize('kw', [

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 evidence for one bench workload, on the GPU box:
-#   tools/profile.sh <tag> [team_battle|rtt] [rollout|step] [fragment]
+#   tools/profile.sh <tag> [team_battle|rtt|maze] [rollout|step] [fragment]
 # 1. --kernel-trace --stats over a bench run (per-kernel durations);
 # 2. two separate --pmc passes, FETCH_SIZE and WRITE_SIZE (they do not fit
 #    one pass on gfx950), over a short run of the same workload.

@@ -11,7 +11,7 @@
                                 stores) -- bench.py reports hbm_bytes_per_launch
                                 as roofline.traffic.
 
-usage: python tools/summarize_profile.py <tag> <team_battle|rtt> --mode rollout|step --raw DIR --dest DIR
+usage: python tools/summarize_profile.py <tag> <team_battle|rtt|maze> --mode rollout|step --raw DIR --dest DIR
 (rollout mode: every step-kernel dispatch is a gw_rollout fragment of
 --fragment steps; the json is pmc_<kernel>_rollout_f<fragment>.json)
 """
@@ -22,7 +22,7 @@ import json
 import os
 import shutil
 
-KERNEL = {'team_battle': 'step_kernel<7>', 'rtt': 'wg_step_kernel<7>'}
+KERNEL = {'team_battle': 'step_kernel<7, 1>', 'rtt': 'wg_step_kernel<7>', 'maze': 'lane_step_kernel<5>'}
 
 
 def find(root, pattern):
