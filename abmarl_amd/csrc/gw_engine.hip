@@ -140,6 +140,7 @@ struct Params {
     // all_done itself), rows of lanes without an observation left unwritten
     int32_t nsteps;
     const uint8_t* ad_in;
+    uint8_t* ad_out;                       // gw_rollout: the last step's __all__ (may alias ad_in)
     int32_t skip_done_obs;
     // observers with different view ranges: slot-geometry (S x S) shadow LUT
     // and static-blocker masks per range (bit wr * S + wc), offsets per range
@@ -2401,6 +2402,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     if (l == 0) {
         p.steps[e] = steps;
         if (p.acting) p.acting[e] = acting_raw + acting_sum;
+        if (p.ad_out) p.ad_out[e] = (uint8_t)prev_all;
     }
     store_lane(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
@@ -3610,7 +3612,7 @@ gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* arg
 }
 
 gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
-                     uint8_t* done, uint8_t* all_done, const uint8_t* all_done_in, uint64_t* acting,
+                     uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint64_t* acting,
                      int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
                      void* stream)
 {
@@ -3621,14 +3623,16 @@ gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32
     Params p = g->base;
     p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
     p.persistent_obs = 0;                  // every step has its own obs slab
-    if (!g->wg && !g->pacman) {
-        // one launch: each env runs its n_steps back to back (step_kernel)
+    if (!g->pacman) {
+        // one launch: each env runs its n_steps back to back (step_kernel,
+        // lane_step_kernel, wg_step_kernel)
         p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
         p.nsteps = n_steps; p.ad_in = all_done_in; p.skip_done_obs = skip_done_obs != 0;
+        p.ad_out = all_done_in;            // each env's wave reads it first, writes it last
         HIPCHK(do_step(g, p, st));
         return GW_OK;
     }
-    // the workgroup and Pacman kernels: one launch per step, __all__ carried
+    // the Pacman kernel: one launch per step, __all__ carried
     // from slab t-1 to slab t (their all_done is in/out)
     const size_t EA = (size_t)g->E * g->A;
     int32_t orows, ocols;
@@ -3647,6 +3651,9 @@ gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32
         p.nsteps = 1; p.ad_in = ad_t;
         HIPCHK(do_step(g, p, st));
     }
+    if (all_done_in)
+        HIPCHK(hipMemcpyAsync(all_done_in, all_done + (size_t)(n_steps - 1) * g->E, (size_t)g->E,
+                              hipMemcpyDeviceToDevice, st));
     return GW_OK;
 }
 

@@ -302,13 +302,19 @@ class GridWorldEngine:
         assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
         assert autoreset in ('same_step', 'next_step'), autoreset
         out = self.rollout_buffers(K) if out is None else out
-        with torch.cuda.device(self.device):
-            _native.check(self.L.gw_rollout(
+        # self.all_done is in/out: gw_rollout leaves the last step's __all__ in it
+        if torch.cuda.current_device() == self.device.index:
+            st = self.L.gw_rollout(
                 self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
                 _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
-                self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream()),
-                'gw_rollout')
-            self.all_done.copy_(out['all_done'][K - 1])
+                self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream())
+        else:
+            with torch.cuda.device(self.device):
+                st = self.L.gw_rollout(
+                    self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                    _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
+                    self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream())
+        _native.check(st, 'gw_rollout')
         self._check_debug('gw_rollout')
         return out
 

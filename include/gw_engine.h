@@ -361,17 +361,21 @@ gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* arg
      obs         device int32[n][E][A][obs shape]
      reward      device double[n][E][A];  done  device uint8[n][E][A]
      all_done    device uint8[n][E]       ('__all__' of every step)
-     all_done_in device uint8[E] or NULL  (the '__all__' before step 0, e.g.
-                 slab n-1 of the previous fragment; NULL = none set)
+     all_done_in device uint8[E] or NULL  (in/out: the '__all__' before step
+                 0, e.g. the previous fragment's; NULL = none set.  Overwritten
+                 with the last step's '__all__' = slab n-1, so consecutive
+                 fragments pass the same buffer)
      acting      device uint64[E] or NULL (+= acting agents over the steps)
    skip_done_obs = 1: obs rows of entities that get no observation in a
    step (done before it, or not grid observers) are left unwritten in that
    step's slab instead of being filled with -2 (the reference returns no obs
-   for them; mask with done).  The workgroup-per-env and Pacman kernels run
-   the fragment as n_steps launches (same results, rows always written).
+   for them; mask with done).  The Pacman kernel runs the fragment as n_steps
+   launches (same results, rows always written); the workgroup-per-env
+   kernel runs it in one launch with the env's state passing through HBM
+   between its steps (rows always written).
    The handle's persistent obs rows (gw_config.persistent_obs) are not used. */
 gw_status gw_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
-                     uint8_t* done, uint8_t* all_done, const uint8_t* all_done_in, uint64_t* acting,
+                     uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint64_t* acting,
                      int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
                      void* stream);
 

@@ -120,12 +120,34 @@ def test_rollout_reach_the_target_double_remove():
 
 def test_rollout_workgroup_kernel():
     """The workgroup-per-env kernel (BASELINE config 4 at 64 envs): the
-    fragment runs as one launch per step, same results."""
+    fragment runs in one launch (each env's state passes through HBM between
+    its steps), same results as single steps, both auto-reset modes."""
     kw = {k: v for k, v in RTT_CONFIG4.items() if k != 'kind'}
     cc = build_rtt(dict(kind='rtt', **kw)).compiled()
     a, b = _pair(cc, 64, run=7, stagger=20)
     assert a.wg
-    _compare(a, b, 0, horizon=20, mode='next_step', frags=(12, 12), allow_err=True)
+    _compare(a, b, 0, horizon=20, mode='next_step', frags=(12, 1, 30), allow_err=True)
+    _compare(a, b, 0, horizon=20, mode='same_step', frags=(25,), allow_err=True)
+
+
+def test_rollout_workgroup_kernel_double_remove():
+    """The crowded ReachTheTarget case forced through the workgroup kernel:
+    the double remove (KeyError) fires inside fragments."""
+    from tests.test_engine_oracle import RTT_WAVE_CASES
+    cc = build_rtt(dict(kind='rtt', **RTT_WAVE_CASES[1])).compiled()
+    a, b = _pair(cc, 256, run=6, force_workgroup=True)
+    assert a.wg
+    _compare(a, b, 0, horizon=40, mode='next_step', frags=(25, 25), allow_err=True)
+    _compare(a, b, 0, horizon=40, mode='same_step', frags=(25,), allow_err=True)
+
+
+def test_rollout_workgroup_team_battle():
+    """TeamBattle with 128 fighters (the workgroup kernel) as fragments."""
+    cc = team_battle(rows=32, cols=32, n_agents=128, n_teams=2)
+    a, b = _pair(cc, 256, run=9, stagger=30)
+    assert a.wg
+    _compare(a, b, 0, horizon=30, mode='next_step', frags=(20, 20))
+    _compare(a, b, 0, horizon=30, mode='same_step', frags=(15,))
 
 
 def test_rollout_traffic_corridor():
