@@ -181,9 +181,34 @@ def quick_config(name, steps=200, warmup=400):
     dt = time.perf_counter() - t0
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     acting = int(eng.acting.sum().item()) - a0
+    roll = None
+    if name != 'pacman':
+        # the same engine as gw_rollout fragments of 100 steps on actions
+        # resident in HBM (the headline line's protocol)
+        F = 100
+        acts = torch.empty((steps,) + tuple(eng.actions.shape), dtype=torch.int32, device=eng.device)
+        for t in range(steps):
+            eng.random_actions(key, warmup + steps + t, out=acts[t])
+        out = eng.rollout_buffers(F)
+        revs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(0, steps, F)]
+        torch.cuda.synchronize()
+        r0 = int(eng.acting.sum().item())
+        t1 = time.perf_counter()
+        for i, ev in zip(range(0, steps, F), revs):
+            ev[0].record()
+            eng.rollout(acts[i:i + F], horizon=horizon, autoreset='next_step', skip_done_obs=True, out=out)
+            ev[1].record()
+        torch.cuda.synchronize()
+        rdt = time.perf_counter() - t1
+        ra = int(eng.acting.sum().item()) - r0
+        roll = {'value': round(ra / rdt, 1), 'ms_per_step': round(rdt / steps * 1e3, 4),
+                'launch_ms': round(float(np.mean([a.elapsed_time(b) for a, b in revs])), 4),
+                'steps_per_launch': F}
     if name == 'maze':
         nbytes = step_bytes(E, eng.A, cc.obs_side)
-        desc = 'MazeNavigation 16x16 (workloads.MAZE_16), 1024 envs, AllStep, next_step auto-reset'
+        desc = ('MazeNavigation 16x16 (workloads.MAZE_16), 1024 envs, AllStep, next_step auto-reset '
+                '(one-lane-per-env kernel)')
     elif name.startswith('rtt'):
         nbytes = rtt_step_bytes(E, eng.A, cc.obs_side, eng.act_dim)
         desc = (f'ReachTheTarget 64x64, 128 barriers + 127 runners + target (256 entities, '
@@ -195,9 +220,11 @@ def quick_config(name, steps=200, warmup=400):
         desc = ('Pacman pacman.txt, 4 baddies + pacman, 16384 envs, TurnBasedManager protocol '
                 '(one agent acts per env per call), next_step auto-reset')
     return {'workload': desc, 'value': round(acting / dt, 1), 'unit': 'agent-steps/s',
+            'protocol': 'one step launch per step (closed loop), Philox action kernel in the timed region',
             'env_steps_per_s': round(E * steps / dt, 1), 'ms_per_step': round(dt / steps * 1e3, 4),
             'kernel_ms': round(kms, 4), 'bytes_per_launch': nbytes,
-            'achieved_GBs': round(nbytes / (kms * 1e-3) / 1e9, 2)}
+            'achieved_GBs': round(nbytes / (kms * 1e-3) / 1e9, 2),
+            'rollout': roll}
 
 
 WORKLOADS = {
