@@ -169,6 +169,7 @@ class CompiledConfig:
         # per-entity observation shape (gw_obs_shape)
         self.obs_shape = (rows, cols) if obs_kind == GW_OBS_ABSOLUTE else (self.obs_side,) * 2
         self.specs = list(specs)
+        self.randomize_placement_order = False
         self.attack_kind = attack_kind
 
     @property

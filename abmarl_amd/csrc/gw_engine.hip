@@ -141,6 +141,9 @@ struct Params {
     int32_t nsteps;
     const uint8_t* ad_in;
     uint8_t* ad_out;                       // gw_rollout: the last step's __all__ (may alias ad_in)
+    // PositionState(randomize_placement_order=True): per env, the lanes in
+    // placement order ([E][A], gw_set_placement_order; NULL = lane order)
+    const int32_t* place_order;
     int32_t skip_done_obs;
     // observers with different view ranges: slot-geometry (S x S) shadow LUT
     // and static-blocker masks per range (bit wr * S + wc), offsets per range
@@ -1609,8 +1612,11 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint32_t remeff = 0;             // lists this lane's placement shortened
         uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)NF : 0u;
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
+        // randomize_placement_order: the shuffled agents dict's order
+        const int32_t* order = p.place_order ? p.place_order + (size_t)blockIdx.x * A : nullptr;
         for (int pass = 0; pass < 2; pass++) {
-            for (int a = 0; a < A; a++) {
+            for (int k = 0; k < A; k++) {
+                const int a = order ? (int)uni(order[k]) : k;
 #ifdef GW_STAMPS
                 uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1914,6 +1920,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
     };
 
     auto place = [&]() -> bool {
+        // the Jacobi form solves lane order only: a shuffled order runs serially
+        if (p.place_order) return position_reset_lanes();
         const int r = position_reset_jacobi();
         if (r == 2) return position_reset_lanes();
         return r == 0;
@@ -2691,6 +2699,7 @@ struct gw_engine {
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
     bool lane_envs;            // lane_step_kernel<S>: MazeNavigation, one lane per env (gw_lane.inc)
+    int32_t* d_place_order;    // gw_set_placement_order: [E][A]
     size_t smem_lane;          // its dynamic LDS: the per-config tables
     PolicySpec policy;
     size_t smem_step, smem_reset;
@@ -3329,6 +3338,7 @@ gw_status gw_destroy(gw_handle g)
     (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
     (void)hipFree(g->d_passive); (void)hipFree(g->d_passive_enc);
     (void)hipFree(g->d_hshadow); (void)hipFree(g->d_hsmask);
+    (void)hipFree(g->d_place_order);
     delete g;
     return GW_OK;
 }
@@ -3342,6 +3352,31 @@ int32_t gw_env_kernel(gw_handle g)
                    : g->lane_envs ? GW_KERNEL_LANE : GW_KERNEL_WAVE;
 }
 int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
+
+gw_status gw_set_placement_order(gw_handle g, const int32_t* lane_order, int32_t n)
+{
+    if (!g) return GW_E_INVALID;
+    if (n == 0 || !lane_order) { g->base.place_order = nullptr; return GW_OK; }
+    if (n != g->E * g->A) { set_err("placement order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
+    if (g->wg || g->pacman) {
+        set_err("randomize_placement_order runs on the one-wave kernel only");
+        return GW_E_UNSUPPORTED;
+    }
+    for (int e = 0; e < g->E; e++) {                 // a permutation of the lanes per env
+        std::vector<uint8_t> seen(g->A, 0);
+        for (int k = 0; k < g->A; k++) {
+            const int32_t a = lane_order[(size_t)e * g->A + k];
+            if (a < 0 || a >= g->A || seen[a]) { set_err("placement order of env %d is not a permutation", e); return GW_E_INVALID; }
+            seen[a] = 1;
+        }
+    }
+    if (!g->d_place_order) HIPCHK(hipMalloc(&g->d_place_order, (size_t)g->E * g->A * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(g->d_place_order, lane_order, (size_t)g->E * g->A * sizeof(int32_t), hipMemcpyHostToDevice));
+    g->base.place_order = g->d_place_order;
+    // the one-lane-per-env maze kernel places in lane order: use the one-wave kernel
+    g->lane_envs = false;
+    return GW_OK;
+}
 
 gw_status gw_lane_entities(gw_handle g, int32_t* out)
 {

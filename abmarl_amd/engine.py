@@ -280,6 +280,17 @@ class GridWorldEngine:
         self.component(_abi.GW_OP_OBSERVE, lane, obs=self.obs)
         return self.obs[:, lane]
 
+    def set_placement_order(self, lane_order):
+        """The lane order the next resets place in, per env (int[E][A]; None
+        = agents-dict order): PositionState(randomize_placement_order=True)."""
+        if lane_order is None:
+            _native.check(self.L.gw_set_placement_order(self.h, None, 0), 'gw_set_placement_order')
+            return
+        o = np.ascontiguousarray(np.asarray(lane_order, dtype=np.int32).reshape(self.E, self.A))
+        _native.check(self.L.gw_set_placement_order(self.h, o.ctypes.data_as(C.c_void_p), o.size),
+                      'gw_set_placement_order')
+        self.kernel = int(self.L.gw_env_kernel(self.h))
+
     def rollout_buffers(self, n_steps):
         """Per-step output slabs for rollout(): obs[n][E][A][...], reward[n][E][A],
         done[n][E][A], all_done[n][E]."""

@@ -91,9 +91,6 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
         raise UnsupportedConfig("exactly one PositionState is required")
     if any(isinstance(a, HealthAgent) for a in agents) and not health_states:
         raise UnsupportedConfig("HealthAgents require a HealthState")
-    if pos_states[0].randomize_placement_order:
-        raise UnsupportedConfig("randomize_placement_order (Python random.shuffle) is not "
-                                "reproduced by the engine")
 
     obs_range = 0
     observe_self = True
@@ -178,7 +175,7 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
     specs = [agent_spec(a, program_type, food_type) for a in agents]
     for i, s in enumerate(specs):
         s.done_target, s.destroy_target = done_target[i], destroy_target[i]
-    return _abi.CompiledConfig(
+    cc = _abi.CompiledConfig(
         sim.grid.rows, sim.grid.cols, specs,
         program,
         sim.grid.overlap_bits(), amap, stacked_attacks=stacked, observe_self=observe_self,
@@ -186,3 +183,9 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
         done_kind=done_kind, obs_range=obs_range, nav_agent=nav_agent, target_agent=target_agent,
         attack_kind=attack_kind, obs_kind=obs_kind, pacman_agent=pacman_agent, tunnel=tunnel,
         pac_rewards=pac_rewards)
+    # PositionState(randomize_placement_order=True) (state.py:97-101): the
+    # host shuffles with Python's random before each reset, exactly as the
+    # reference does, and hands the order to the engine
+    # (gw_set_placement_order; the dict-level API, one env per runtime)
+    cc.randomize_placement_order = bool(pos_states[0].randomize_placement_order)
+    return cc

@@ -14,6 +14,7 @@ space assignment.  They run on the engine two ways:
 Reference: abmarl/sim/gridworld/state.py:13-166,622-641; actor.py:13-114,
 237-501; observer.py:13-52,153-250; done.py:10-153.
 """
+import random
 from abc import ABC, abstractmethod
 
 import numpy as np
@@ -56,11 +57,14 @@ class PositionState(StateBaseComponent):
 
     def reset(self, **kwargs):
         """Grid.reset, then every agent placed (gw_component POSITION_RESET)."""
+        rt = ComponentRuntime.of(self)
         if self.randomize_placement_order:
-            raise NotImplementedError("randomize_placement_order (Python random.shuffle) is not "
-                                      "reproduced by the engine")
-        status, _, err = ComponentRuntime.of(self).op(
-            _abi.GW_OP_POSITION_RESET, args=[int(self.no_overlap_at_reset)])
+            # state.py:97-101: random.shuffle of the agents dict's items, kept
+            # for the next reset (Python's own random: the reference's draws)
+            items = self.__dict__.setdefault('_place_items', list(self.agents))
+            random.shuffle(items)
+            rt.eng.set_placement_order([rt.index[aid] for aid in items])
+        status, _, err = rt.op(_abi.GW_OP_POSITION_RESET, args=[int(self.no_overlap_at_reset)])
         if err & _abi.GW_ERR_INIT_POSITION:
             raise AssertionError("Cell is not available for an agent with an initial position.")
         if err & _abi.GW_ERR_NO_CELL or not status:

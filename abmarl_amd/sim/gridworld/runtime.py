@@ -9,6 +9,8 @@ Every reset/step:
 So ``np.random.seed(s); manager.reset(); manager.step(...)`` consumes and
 produces exactly what the reference does for the same seed.
 """
+import random
+
 import numpy as np
 import torch
 
@@ -47,6 +49,9 @@ class DictRuntime:
         self.sides = [2 * a.view_range + 1 if isinstance(a, GridObservingAgent) else 0
                       for a in sim.agents.values()]
         self.lazy = compiled.cfg.sim_kind == _abi.GW_SIM_PACMAN
+        # PositionState(randomize_placement_order=True): the component's own
+        # agents dict, reshuffled in place at every reset (state.py:97-101)
+        self.place_items = list(range(len(self.ids))) if compiled.randomize_placement_order else None
         if self.lazy:
             self.key = 'absolute_encoding'
             specs = compiled.specs
@@ -105,7 +110,17 @@ class DictRuntime:
             self.eng.set_aux_state(racc=torch.as_tensor(self.racc[None], device=self.dev))
             self._racc_dirty = False
 
+    def _shuffle_placement(self):
+        """random.shuffle of the PositionState's agents dict, as the reference
+        does it (Python's own random: the same draws), then the lanes in that
+        order to the engine (static entities overlap nothing: left out)."""
+        if self.place_items is None:
+            return
+        random.shuffle(self.place_items)
+        self.eng.set_placement_order([int(self.lane_of[i]) for i in self.place_items if self.lane_of[i] >= 0])
+
     def _lazy_reset(self):
+        self._shuffle_placement()
         self._push_rng()
         self.eng.err.zero_()
         self.eng.sim_reset()
@@ -145,6 +160,7 @@ class DictRuntime:
     def reset(self):
         if self.lazy:
             return self._lazy_reset()
+        self._shuffle_placement()
         self._push_rng()
         self.eng.err.zero_()
         obs = self.eng.reset()

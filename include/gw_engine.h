@@ -437,6 +437,14 @@ gw_status gw_set_aux_state(gw_handle h, const double* racc, const uint32_t* pass
 
 gw_status gw_destroy(gw_handle h);
 
+/* PositionState(randomize_placement_order=True) (state.py:97-101): the
+   order in which the next resets place each env's lanes, lane_order[E][A]
+   (host memory; a permutation of 0..A-1 per env: the shuffled agents dict,
+   static entities left out -- they overlap nothing, so their place in the
+   order changes nothing).  n = 0 restores agents-dict order.  One-wave
+   kernel only (a MazeNavigation handle leaves the one-lane kernel).       */
+gw_status gw_set_placement_order(gw_handle h, const int32_t* lane_order, int32_t n);
+
 /* Introspection */
 int32_t     gw_num_envs(gw_handle h);
 int32_t     gw_obs_side(gw_handle h);

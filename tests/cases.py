@@ -115,6 +115,7 @@ def build_sim(c, sim_cls=None):
         attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
         stacked_attacks=c['stacked_attacks'], observe_self=c['observe_self'],
         no_overlap_at_reset=c['no_overlap_at_reset'],
+        randomize_placement_order=c.get('randomize_placement_order', False),
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
         dones=set(c.get('dones', ['OneTeamRemainingDone'])), state_order=c['state_order'])

@@ -135,6 +135,13 @@ CASES = [
          stacked_attacks=True, observe_self=False,
          agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=0.8,
                     view_range=2, simultaneous_attacks=2)),
+    # PositionState(randomize_placement_order=True): Python's random.shuffle of
+    # the agents dict before every placement (state.py:97-101), shared initial
+    # cells within a team so the shuffled insertion order shows in the
+    # crowded-cell draws; per-env Python random streams (py_seeds)
+    dict(name='tb_shuffle', rows=8, cols=8, n_agents=12, n_teams=2, n_envs=4, n_steps=150,
+         horizon=30, seed_base=55, randomize_placement_order=True,
+         initial_positions={0: [0, 0], 2: [0, 0], 5: [3, 3], 7: [3, 3]}),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
@@ -194,6 +201,9 @@ def full_case(case):
     c.setdefault('initial_health', {})
     c.setdefault('agent', DEFAULT_AGENT)
     c.setdefault('dones', ['OneTeamRemainingDone'])
+    c.setdefault('randomize_placement_order', False)
+    if c['randomize_placement_order']:
+        c['py_seeds'] = [(c['seed_base'] * 7919 + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
     if 'target_mapping' in c:
         c['target_mapping'] = {f'agent{k}': f'agent{v}' for k, v in c['target_mapping'].items()}
     if c.pop('corners', False):
@@ -332,6 +342,7 @@ def build_reference_env(c):
         stacked_attacks=c['stacked_attacks'],
         observe_self=c['observe_self'],
         no_overlap_at_reset=c['no_overlap_at_reset'],
+        randomize_placement_order=c.get('randomize_placement_order', False),
         states={'PositionState', 'HealthState'},
         observers={'PositionCenteredEncodingObserver'},
         dones=set(c['dones']))
@@ -375,13 +386,17 @@ def run_case(case):
                 ret[i] = 1
         return out, ret
 
-    rng_states = []
+    import random
+    rng_states, py_states = [], []
     obs0 = np.zeros((E, A, S, S), dtype=np.int8)
     for e in range(E):
         np.random.seed(c['seeds'][e])
+        if 'py_seeds' in c:                 # Python's random: randomize_placement_order
+            random.seed(c['py_seeds'][e])
         o = managers[e].reset()
         obs0[e], _ = obs_array(o)
         rng_states.append(np.random.get_state())
+        py_states.append(random.getstate())
 
     out = dict(
         obs=np.zeros((T, E, A, S, S), dtype=np.int8),
@@ -403,6 +418,7 @@ def run_case(case):
         for e in range(E):
             m = managers[e]
             np.random.set_state(rng_states[e])
+            random.setstate(py_states[e])
             adict = {}
             for i, aid in enumerate(ids):
                 if aid not in m.done_agents:
@@ -435,6 +451,7 @@ def run_case(case):
                 out['reset_mask'][t, e] = 1
                 out['reset_obs'][t, e], _ = obs_array(ro)
                 rng_states[e] = np.random.get_state()
+                py_states[e] = random.getstate()
                 continue
             steps[e] += 1
             out['obs'][t, e], out['returned'][t, e] = obs_array(o)
@@ -456,6 +473,7 @@ def run_case(case):
                 out['reset_mask'][t, e] = 1
                 out['reset_obs'][t, e], _ = obs_array(ro)
             rng_states[e] = np.random.get_state()
+            py_states[e] = random.getstate()
     path = os.path.join(HERE, c['name'] + '.npz')
     np.savez_compressed(path, case=json.dumps(c), actions=act, obs0=obs0, **out)
     print(f"{c['name']}: {T} steps x {E} envs x {A} entities, resets={int(out['reset_mask'].sum())}, "

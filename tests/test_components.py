@@ -35,6 +35,36 @@ KEY = 'position_centered_encoding'
 
 # ------------------------------------------------------------------ states
 @gpu
+def test_position_state_randomize_placement_order():
+    """state.py:97-101: random.shuffle of the agents dict before every
+    placement; known answers from the reference itself
+    (tests/golden/make_shuffle_known_answers.py: six resets after
+    random.seed(3), np.random.seed(5)), cell insertion order included, and
+    both RNG streams left where the reference leaves them."""
+    import random
+    agents = {'a0': GridWorldAgent(id='a0', encoding=1), 'a1': GridWorldAgent(id='a1', encoding=2),
+              'a2': GridWorldAgent(id='a2', encoding=1, initial_position=np.array([0, 0])),
+              'a3': GridWorldAgent(id='a3', encoding=2), 'a4': GridWorldAgent(id='a4', encoding=1)}
+    grid = Grid(2, 3, overlapping={1: {1}})
+    state = PositionState(grid=grid, agents=agents, randomize_placement_order=True)
+    ref = [[[1, 0], [0, 2], [0, 0], [1, 1], [0, 0], ['a2', 'a4']],
+           [[1, 0], [0, 1], [0, 0], [1, 2], [0, 0], ['a2', 'a4']],
+           [[0, 1], [1, 2], [0, 0], [1, 1], [0, 0], ['a2', 'a4']],
+           [[0, 0], [1, 1], [0, 0], [0, 1], [1, 2], ['a2', 'a0']],
+           [[1, 2], [1, 1], [0, 0], [0, 2], [0, 1], ['a2']],
+           [[0, 1], [1, 0], [0, 0], [1, 2], [0, 1], ['a2']]]
+    random.seed(3)
+    np.random.seed(5)
+    for k, want in enumerate(ref):
+        state.reset()
+        got = [list(map(int, agents[a].position)) for a in ['a0', 'a1', 'a2', 'a3', 'a4']]
+        assert got == want[:5], (k, got, want)
+        assert list(grid[0, 0]) == want[5], (k, list(grid[0, 0]))
+    assert np.random.get_state()[2] == 38
+    assert random.random() == 0.6714114753695926
+
+
+@gpu
 def test_position_state_initial_positions():
     """test_state.py:11-28."""
     grid = Grid(3, 3)

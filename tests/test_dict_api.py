@@ -2,6 +2,7 @@
 np.random.seed(s) + AllStepManager(TeamBattleSim...) reset/step dicts match
 the reference's trajectories (golden fixtures) exactly, and the global
 np.random stream ends in the same state (position + key digest)."""
+import random
 import zlib
 
 import numpy as np
@@ -34,7 +35,8 @@ def _action(agent, a):
 
 
 @pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners', 'tb_walls',
-                                  'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double'])
+                                  'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double',
+                                  'tb_shuffle'])
 def test_dict_api_matches_reference(name):
     g = load_golden(name)
     c = g['case']
@@ -45,6 +47,8 @@ def test_dict_api_matches_reference(name):
         agents0 = np.array([isinstance(a, Agent) for a in sim.agents.values()])
         env = MultiAgentWrapper(AllStepManager(sim))
         np.random.seed(c['seeds'][e])
+        if 'py_seeds' in c:            # PositionState(randomize_placement_order=True)
+            random.seed(c['py_seeds'][e])
         obs = env.reset()
         _check_obs(obs, g['obs0'][e], agents0, index)
         for t in range(g['actions'].shape[0]):
@@ -116,3 +120,4 @@ def test_batched_env_next_step_autoreset():
         steps = env.engine.get_state()['steps'].cpu().numpy()
         prev_all = (a != 0) | (steps >= 15)
     assert seen > 64
+

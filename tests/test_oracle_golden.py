@@ -40,3 +40,22 @@ def test_oracle_matches_reference(oracle_mod, name):
     g = load_golden(name)
     n = replay(OracleRunner(oracle_mod, g), g)
     assert n == g['actions'].shape[0]
+
+
+def test_shuffle_fixture_needs_the_shuffle(oracle_mod):
+    """tb_shuffle (PositionState(randomize_placement_order=True), replayed on
+    the GPU through the dict API by test_dict_api.py) is evidence only if the
+    shuffled order changes the outcome: placing in agents-dict order from the
+    same numpy seeds gives other first observations."""
+    import json
+    g = load_golden('tb_shuffle')
+    c = dict(g['case'])
+    c['randomize_placement_order'] = False
+    from tests.cases import build_sim
+    cc = build_sim(c).compiled()
+    o = oracle_mod.Oracle(cc, c['n_envs'])
+    o.seed(c['seeds'])
+    obs = o.new_obs()
+    o.reset(obs)
+    assert (obs != g['obs0']).any()
+    assert json.loads(json.dumps(g['case']))['randomize_placement_order'] is True
