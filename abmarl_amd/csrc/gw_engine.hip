@@ -144,6 +144,11 @@ struct Params {
     // PositionState(randomize_placement_order=True): per env, the lanes in
     // placement order ([E][A], gw_set_placement_order; NULL = lane order)
     const int32_t* place_order;
+    // AllStepManager(randomize_action_input=True): per env, the lanes in
+    // action-dict order and each lane's rank in it ([E][A] each,
+    // gw_set_action_order; NULL = agents-dict order).  Generic kernel only.
+    const int32_t* act_order;
+    const int32_t* act_rank;
     int32_t skip_done_obs;
     // observers with different view ranges: slot-geometry (S x S) shadow LUT
     // and static-blocker masks per range (bit wr * S + wc), offsets per range
@@ -2115,6 +2120,10 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             bool raised = false;                 // ReachTheTarget's double remove (KeyError)
 
             if (sim_kind == GW_SIM_TEAM_BATTLE) {
+                // AllStepManager(randomize_action_input=True): the shuffled
+                // action dict's order (the generic kernel only)
+                const int32_t* aord = (!PLAIN && p.act_order) ? p.act_order + (size_t)e * A : nullptr;
+                const int my_rank = (!PLAIN && p.act_order) ? p.act_rank[(size_t)e * A + (valid ? l : 0)] : l;
                 // ---- attack pass (team_battle_example.py:35-47)
                 const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
                 const bool maybe = att && L.active && attack_precheck(p, sm, L);
@@ -2139,14 +2148,14 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // just before the next serial attacker after them (so each lane's
                 // reward terms keep their reference order), or after the loop.
                 uint64_t pend = __ballot(att) & ~maybe_mask;
-                for (uint64_t it = maybe_mask; it; it &= it - 1) {
-                    const int a = first_lane(it);
-                    const uint64_t before = pend & ((1ull << a) - 1ull);
+                // one serial attacker; `before`: the pending lanes whose turn
+                // came before a's
+                auto serial_attack = [&](int a, uint64_t before) {
                     if (before) {
                         if (((before >> l) & 1ull) && L.active) L.reward -= 0.1;
                         pend &= ~before;
                     }
-                    if (!rlb(L.active, a)) continue;                // killed earlier this pass
+                    if (!rlb(L.active, a)) return;                  // killed earlier this pass
                     int nlist, list;
                     attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
@@ -2158,6 +2167,18 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                                 if (l == a) L.reward += 1.0;
                             }
                         }
+                    }
+                };
+                if (aord) {
+                    // randomize_action_input: the action dict's order
+                    for (int k = 0; k < A; k++) {
+                        const int a = uni(aord[k]);
+                        if ((maybe_mask >> a) & 1ull) serial_attack(a, pend & __ballot(valid && my_rank < k));
+                    }
+                } else {
+                    for (uint64_t it = maybe_mask; it; it &= it - 1) {
+                        const int a = first_lane(it);
+                        serial_attack(a, pend & ((1ull << a) - 1ull));
                     }
                 }
                 if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
@@ -2188,7 +2209,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 }
                 const int pr = L.r, pc = L.c;
                 bool moved = false;
-                if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)l; moved = true; }
+                if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)my_rank; moved = true; }
                 bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
         #ifdef GW_STAMPS
                 {
@@ -2197,10 +2218,22 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 }
         #endif
                 STAMP(11);
-                for (uint64_t it = __ballot(real && !iso); it; it &= it - 1) {
-                    const int a = first_lane(it);
-                    const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
-                    if (l == a) { fail = !ok; moved = ok; }
+                const uint64_t ser = __ballot(real && !iso);
+                if (aord) {
+                    // randomize_action_input: movers in the action dict's
+                    // order, appended to their cells in that order
+                    for (int k = 0; k < A; k++) {
+                        const int a = uni(aord[k]);
+                        if (!((ser >> a) & 1ull)) continue;
+                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)k);
+                        if (l == a) { fail = !ok; moved = ok; }
+                    }
+                } else {
+                    for (uint64_t it = ser; it; it &= it - 1) {
+                        const int a = first_lane(it);
+                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                        if (l == a) { fail = !ok; moved = ok; }
+                    }
                 }
                 if (fail) L.reward -= 0.1;
                 ctr += (uint32_t)WAVE;
@@ -2700,6 +2733,7 @@ struct gw_engine {
     bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
     bool lane_envs;            // lane_step_kernel<S>: MazeNavigation, one lane per env (gw_lane.inc)
     int32_t* d_place_order;    // gw_set_placement_order: [E][A]
+    int32_t* d_act_order;      // gw_set_action_order: order [E][A] | rank [E][A]
     size_t smem_lane;          // its dynamic LDS: the per-config tables
     PolicySpec policy;
     size_t smem_step, smem_reset;
@@ -2800,7 +2834,9 @@ static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
     if (g->lane_envs) return part_launch(g, PK_STEP_LANE, g->smem_lane, p, st);
-    return part_launch(g, g->wg ? PK_WG_STEP : (g->step_tb ? PK_STEP_TB : PK_STEP), g->smem_step, p, st);
+    // an action order other than the agents dict's runs on the generic kernel
+    const bool tb = g->step_tb && !p.act_order;
+    return part_launch(g, g->wg ? PK_WG_STEP : (tb ? PK_STEP_TB : PK_STEP), g->smem_step, p, st);
 }
 
 static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
@@ -3338,7 +3374,7 @@ gw_status gw_destroy(gw_handle g)
     (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
     (void)hipFree(g->d_passive); (void)hipFree(g->d_passive_enc);
     (void)hipFree(g->d_hshadow); (void)hipFree(g->d_hsmask);
-    (void)hipFree(g->d_place_order);
+    (void)hipFree(g->d_place_order); (void)hipFree(g->d_act_order);
     delete g;
     return GW_OK;
 }
@@ -3352,6 +3388,33 @@ int32_t gw_env_kernel(gw_handle g)
                    : g->lane_envs ? GW_KERNEL_LANE : GW_KERNEL_WAVE;
 }
 int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
+
+gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
+{
+    if (!g) return GW_E_INVALID;
+    if (n == 0 || !lane_order) { g->base.act_order = nullptr; g->base.act_rank = nullptr; return GW_OK; }
+    if (n != g->E * g->A) { set_err("action order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
+    if (g->wg || g->pacman || g->lane_envs || g->base.sim_kind != GW_SIM_TEAM_BATTLE) {
+        set_err("randomize_action_input runs with the TeamBattle program on the one-wave kernel only");
+        return GW_E_UNSUPPORTED;
+    }
+    std::vector<int32_t> both((size_t)2 * g->E * g->A);
+    for (int e = 0; e < g->E; e++) {
+        std::vector<uint8_t> seen(g->A, 0);
+        for (int k = 0; k < g->A; k++) {
+            const int32_t a = lane_order[(size_t)e * g->A + k];
+            if (a < 0 || a >= g->A || seen[a]) { set_err("action order of env %d is not a permutation", e); return GW_E_INVALID; }
+            seen[a] = 1;
+            both[(size_t)e * g->A + k] = a;
+            both[(size_t)g->E * g->A + (size_t)e * g->A + a] = k;
+        }
+    }
+    if (!g->d_act_order) HIPCHK(hipMalloc(&g->d_act_order, both.size() * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(g->d_act_order, both.data(), both.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    g->base.act_order = g->d_act_order;
+    g->base.act_rank = g->d_act_order + (size_t)g->E * g->A;
+    return GW_OK;
+}
 
 gw_status gw_set_placement_order(gw_handle g, const int32_t* lane_order, int32_t n)
 {

@@ -291,6 +291,17 @@ class GridWorldEngine:
                       'gw_set_placement_order')
         self.kernel = int(self.L.gw_env_kernel(self.h))
 
+    def set_action_order(self, lane_order):
+        """The lane order of the action dict the next steps process, per env
+        (int[E][A]; None = agents-dict order):
+        AllStepManager(randomize_action_input=True)."""
+        if lane_order is None:
+            _native.check(self.L.gw_set_action_order(self.h, None, 0), 'gw_set_action_order')
+            return
+        o = np.ascontiguousarray(np.asarray(lane_order, dtype=np.int32).reshape(self.E, self.A))
+        _native.check(self.L.gw_set_action_order(self.h, o.ctypes.data_as(C.c_void_p), o.size),
+                      'gw_set_action_order')
+
     def rollout_buffers(self, n_steps):
         """Per-step output slabs for rollout(): obs[n][E][A][...], reward[n][E][A],
         done[n][E][A], all_done[n][E]."""

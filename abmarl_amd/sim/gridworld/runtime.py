@@ -174,11 +174,22 @@ class DictRuntime:
     def step(self, action_dict):
         ids = [a for a in action_dict]
         order = [self.index[a] for a in ids]
-        if order != sorted(order):
+        shuffled = order != sorted(order)
+        if shuffled and (self.lazy or self.cc.cfg.sim_kind != _abi.GW_SIM_TEAM_BATTLE):
             raise NotImplementedError(
-                "the engine processes actions in agents-dict order; got a different order")
+                "an action dict in another order than the agents dict (randomize_action_input) "
+                "runs with the TeamBattle program only")
         if self.lazy:
             return self._lazy_step(action_dict)
+        # AllStepManager(randomize_action_input=True): the shuffled dict's order
+        if shuffled:
+            first = [int(self.lane_of[i]) for i in order if self.lane_of[i] >= 0]
+            rest = [k for k in range(len(self.lanes)) if k not in set(first)]
+            self.eng.set_action_order(first + rest)
+            self._act_order_set = True
+        elif getattr(self, '_act_order_set', False):
+            self.eng.set_action_order(None)
+            self._act_order_set = False
         act = np.zeros((1, len(self.lanes), self.eng.act_dim), np.int32)
         act[0, :, 2] = -1                      # not in action_dict: does not act
         for aid, a in action_dict.items():

@@ -445,6 +445,15 @@ gw_status gw_destroy(gw_handle h);
    kernel only (a MazeNavigation handle leaves the one-lane kernel).       */
 gw_status gw_set_placement_order(gw_handle h, const int32_t* lane_order, int32_t n);
 
+/* AllStepManager(randomize_action_input=True) (all_step_manager.py:62-65):
+   the order of the action dict the next steps process, lane_order[E][A]
+   (host memory; per env a permutation of 0..A-1: the lanes in the shuffled
+   dict first, the others after).  The TeamBattle program's attack and move
+   passes go in that order (team_battle_example.py:33-59) and movers enter
+   their cells in it.  n = 0 restores agents-dict order.  One-wave kernel,
+   TeamBattle program only.                                                  */
+gw_status gw_set_action_order(gw_handle h, const int32_t* lane_order, int32_t n);
+
 /* Introspection */
 int32_t     gw_num_envs(gw_handle h);
 int32_t     gw_obs_side(gw_handle h);

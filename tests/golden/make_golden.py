@@ -142,6 +142,14 @@ CASES = [
     dict(name='tb_shuffle', rows=8, cols=8, n_agents=12, n_teams=2, n_envs=4, n_steps=150,
          horizon=30, seed_base=55, randomize_placement_order=True,
          initial_positions={0: [0, 0], 2: [0, 0], 5: [3, 3], 7: [3, 3]}),
+    # AllStepManager(randomize_action_input=True): the action dict shuffled
+    # with Python's random every step (all_step_manager.py:62-65), so the
+    # attack and move passes run in that order; dense, accuracy < 1
+    dict(name='tb_shuffle_act', rows=7, cols=7, n_agents=16, n_teams=2, n_envs=4, n_steps=150,
+         horizon=40, seed_base=57, randomize_action_input=True,
+         overlap={1: [1, 2], 2: [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.6, attack_accuracy=0.7,
+                    view_range=2)),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
@@ -202,7 +210,8 @@ def full_case(case):
     c.setdefault('agent', DEFAULT_AGENT)
     c.setdefault('dones', ['OneTeamRemainingDone'])
     c.setdefault('randomize_placement_order', False)
-    if c['randomize_placement_order']:
+    c.setdefault('randomize_action_input', False)
+    if c['randomize_placement_order'] or c['randomize_action_input']:
         c['py_seeds'] = [(c['seed_base'] * 7919 + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
     if 'target_mapping' in c:
         c['target_mapping'] = {f'agent{k}': f'agent{v}' for k, v in c['target_mapping'].items()}
@@ -362,7 +371,7 @@ def build_reference_env(c):
     pos = [s for s in sim._states if isinstance(s, PositionState)][0]
     hea = [s for s in sim._states if isinstance(s, HealthState)][0]
     sim._states = [pos, hea] if c['state_order'] == 'position_health' else [hea, pos]
-    return AllStepManager(sim)
+    return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
 def run_case(case):

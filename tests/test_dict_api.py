@@ -36,7 +36,7 @@ def _action(agent, a):
 
 @pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners', 'tb_walls',
                                   'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double',
-                                  'tb_shuffle'])
+                                  'tb_shuffle', 'tb_shuffle_act'])
 def test_dict_api_matches_reference(name):
     g = load_golden(name)
     c = g['case']
@@ -45,7 +45,8 @@ def test_dict_api_matches_reference(name):
         ids = list(sim.agents)
         index = {k: i for i, k in enumerate(ids)}
         agents0 = np.array([isinstance(a, Agent) for a in sim.agents.values()])
-        env = MultiAgentWrapper(AllStepManager(sim))
+        env = MultiAgentWrapper(AllStepManager(
+            sim, randomize_action_input=bool(c.get('randomize_action_input', False))))
         np.random.seed(c['seeds'][e])
         if 'py_seeds' in c:            # PositionState(randomize_placement_order=True)
             random.seed(c['py_seeds'][e])

@@ -59,3 +59,14 @@ def test_shuffle_fixture_needs_the_shuffle(oracle_mod):
     o.reset(obs)
     assert (obs != g['obs0']).any()
     assert json.loads(json.dumps(g['case']))['randomize_placement_order'] is True
+
+
+def test_shuffled_action_fixture_needs_the_shuffle(oracle_mod):
+    """tb_shuffle_act (AllStepManager(randomize_action_input=True), replayed
+    on the GPU through the dict API by test_dict_api.py) is evidence only if
+    the shuffled action order changes the trajectory: the agents-dict order
+    from the same seeds and actions diverges from it."""
+    g = load_golden('tb_shuffle_act')
+    assert g['case']['randomize_action_input'] is True
+    with pytest.raises(AssertionError):
+        replay(OracleRunner(oracle_mod, g), g)
