@@ -59,6 +59,11 @@ def lib():
         L.gwo_observe.argtypes = [vp, C.c_int32, vp]
         L.gwo_get_aux.argtypes = [vp, vp, vp, vp]
         L.gwo_take_reward.argtypes = [vp, C.c_int32, vp]
+        L.gwo_generate_maze.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp]
+        L.gwo_pyset_order.argtypes = [vp, C.c_int32, C.c_int32, vp]
+        L.gwo_maze_place.restype = C.c_uint32
+        L.gwo_maze_place.argtypes = [vp, C.c_int32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32,
+                                     C.c_int32, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -176,3 +181,44 @@ def mt_probe(seed, kind, arg, n):
     out = np.zeros(n, np.float64)
     lib().gwo_mt_probe(int(seed), int(kind), int(arg), int(n), _p(out))
     return out
+
+
+def mt_state(seed):
+    """numpy legacy MT19937 state after np.random.seed(seed): key[624] + pos."""
+    st = np.random.RandomState(seed).get_state()
+    mt = np.zeros(_abi.GW_MT_N + 1, np.uint32)
+    mt[:_abi.GW_MT_N] = st[1]
+    mt[_abi.GW_MT_N] = st[2]
+    return mt
+
+
+def generate_maze(rows, cols, start, mt):
+    """generate_maze (utils.py:120-212) on the MT19937 state mt (in/out)."""
+    out = np.zeros((rows, cols), np.int8)
+    sr, sc = (-1, -1) if start is None else (int(start[0]), int(start[1]))
+    lib().gwo_generate_maze(int(rows), int(cols), sr, sc, _p(mt), _p(out))
+    return out
+
+
+def maze_place(compiled, target, barrier, free, mt, cluster=False, scatter=False,
+               no_overlap=False, order=None):
+    """MazePlacementState.reset (state.py:500-619) of every entity of compiled."""
+    n = compiled.n_agents
+    bits = lambda encs: sum(1 << int(e) for e in encs)
+    pos = np.zeros((n, 2), np.int32)
+    seq = np.zeros(n, np.int32)
+    in_grid = np.zeros(n, np.uint8)
+    maze = np.zeros((compiled.rows, compiled.cols), np.int8)
+    o = None if order is None else np.ascontiguousarray(order, np.int32)
+    err = lib().gwo_maze_place(C.cast(C.byref(compiled.cfg), C.c_void_p), int(target), bits(barrier),
+                               bits(free), int(cluster), int(scatter), int(no_overlap), _p(o), _p(mt),
+                               _p(pos), _p(seq), _p(in_grid), _p(maze))
+    return dict(err=int(err), pos=pos, seq=seq, in_grid=in_grid, maze=maze)
+
+
+def pyset_order(cells, cols):
+    """list(set(...)) order of distinct (r, c) tuples given as r * cols + c."""
+    a = np.ascontiguousarray(cells, np.int32)
+    out = np.zeros(len(a), np.int32)
+    lib().gwo_pyset_order(_p(a), len(a), int(cols), _p(out))
+    return out.tolist()
