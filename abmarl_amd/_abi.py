@@ -32,6 +32,7 @@ GW_OP_HEALTH_RESET = 2
 GW_OP_MOVE = 3
 GW_OP_ATTACK = 4
 GW_OP_OBSERVE = 5
+GW_OP_MAZE_RESET = 6
 
 GW_K_OBSERVING = 0x01
 GW_K_ACTING = 0x02

@@ -42,6 +42,7 @@ SIGNATURES = {
                                _vp, _vp]),
     'gw_rollout': (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     'gw_component': (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    'gw_generate_maze': (_i32, [_vp, _vp, _vp, _vp]),
     'gw_destroy': (_i32, [_vp]),
     'gw_num_envs': (_i32, [_vp]),
     'gw_obs_side': (_i32, [_vp]),

@@ -2658,6 +2658,7 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 
 #ifndef GW_PART_S
 #include "gw_pacman.inc"
+#include "gw_maze.inc"
 #endif
 #include "gw_rtt.inc"
 #include "gw_lane.inc"
@@ -2741,6 +2742,7 @@ struct gw_engine {
     bool pacman;
     int16_t* d_passive;        // passive_cell [n_passive] | cell_passive [HW]
     int8_t* d_passive_enc;
+    int32_t n_ent;             // gw_config.n_agents (lanes + static entities)
 };
 
 // create_grid_and_mask (utils.py:46-115): the window cells of range R that a
@@ -3015,6 +3017,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     g->S = pac ? 1 : 2 * cfg->obs_range + 1; g->max_enc = max_enc;
     g->pacman = pac;
     g->wg = wg;
+    g->n_ent = NE;
     for (int i = 0; i < A; i++) g->lane_ent[i] = lanes[i];
     const size_t EA = (size_t)n_envs * A;
     Params& p = g->base;
@@ -3689,13 +3692,50 @@ gw_status gw_rollout_step(gw_handle g, uint64_t key, uint32_t step, uint32_t env
     return GW_OK;
 }
 
+static gw_status maze_launch(gw_engine* g, int mode, const int32_t* args, const int32_t* start, int8_t* maze,
+                             int32_t* result, uint32_t* err_flags, hipStream_t st)
+{
+    if (g->H * g->W > GW_MAX_CELLS || g->H < 1 || g->W < 1) return GW_E_INVALID;
+    MazeCall m;
+    m.mode = mode; m.start = start; m.maze_out = maze;
+    m.T = maze_table_slots(g->H, g->W);
+    const size_t smem = maze_smem_bytes(g->H, g->W, m.T);
+    static bool attr_set = false;
+    if (!attr_set) {
+        HIPCHK(hipFuncSetAttribute((const void*)maze_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024));
+        attr_set = true;
+    }
+    if (smem > 160 * 1024) { set_err("maze: %zu B of LDS per env", smem); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.actions = args; p.comp_out = result; p.err = err_flags;
+    hipLaunchKernelGGL(maze_kernel, dim3(g->E), dim3(WAVE), smem, st, p, m);
+    HIPCHK(hipGetLastError());
+    return GW_OK;
+}
+
+gw_status gw_generate_maze(gw_handle g, const int32_t* start, int8_t* maze, void* stream)
+{
+    if (!g || !maze) return GW_E_INVALID;
+    if (g->pacman) { set_err("generate_maze: not on a Pacman handle"); return GW_E_UNSUPPORTED; }
+    return maze_launch(g, 0, nullptr, start, maze, nullptr, nullptr, (hipStream_t)stream);
+}
+
 gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
                        int32_t* obs, uint32_t* err_flags, void* stream)
 {
-    if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_OBSERVE) return GW_E_INVALID;
+    if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_MAZE_RESET) return GW_E_INVALID;
     if (g->wg || g->pacman) {
         set_err("component operations run on the one-wave engine (not the workgroup / Pacman kernels)");
         return GW_E_UNSUPPORTED;
+    }
+    if (op == GW_OP_MAZE_RESET) {
+        if (!args || g->base.act_dim < 3) return GW_E_INVALID;
+        if (g->n_ent != g->A) {
+            set_err("MazePlacementState places every entity: the handle must hold no static entities (all_lanes)");
+            return GW_E_UNSUPPORTED;
+        }
+        return maze_launch(g, 1, args, nullptr, nullptr, result, err_flags, (hipStream_t)stream);
     }
     const bool needs_lane = op == GW_OP_MOVE || op == GW_OP_ATTACK || op == GW_OP_OBSERVE;
     if (needs_lane && (lane < 0 || lane >= g->A)) { set_err("lane %d outside 0..%d", lane, g->A - 1); return GW_E_INVALID; }

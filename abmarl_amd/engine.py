@@ -254,6 +254,32 @@ class GridWorldEngine:
                                               _ptr(obs), _ptr(self.err), _stream()), 'gw_component')
         return result
 
+    def maze_reset(self, target, barrier_encodings, free_encodings, cluster_barriers=False,
+                   scatter_free_agents=False, no_overlap_at_reset=False, result=None):
+        """MazePlacementState.reset (state.py:500-619) in every env
+        (gw_component GW_OP_MAZE_RESET); returns status int32[E] (1 placed)."""
+        bits = lambda encs: sum(1 << int(x) for x in encs)
+        args = torch.zeros((self.E, self.act_dim), dtype=torch.int32, device=self.device)
+        args[:, 0] = (int(bool(no_overlap_at_reset)) | int(bool(cluster_barriers)) << 1 |
+                      int(bool(scatter_free_agents)) << 2 | int(target) << 8)
+        args[:, 1] = bits(barrier_encodings)
+        args[:, 2] = bits(free_encodings)
+        res = result if result is not None else \
+            torch.zeros((self.E, 2 + self.A), dtype=torch.int32, device=self.device)
+        self.component(_abi.GW_OP_MAZE_RESET, -1, args, res)
+        return res[:, 0]
+
+    def generate_maze(self, start=None, out=None):
+        """generate_maze(rows, cols, start) (utils.py:120-212) in every env on
+        its own np.random stream: int8[E][rows][cols], 0 passage / 1 wall.
+        start: int32[E][2] device tensor (a negative row = None) or None."""
+        H, W = self.cc.rows, self.cc.cols
+        out = out if out is not None else torch.empty((self.E, H, W), dtype=torch.int8, device=self.device)
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_generate_maze(self.h, _ptr(start), _ptr(out), _stream()),
+                          'gw_generate_maze')
+        return out
+
     def move(self, lane, moves):
         """MoveActor.process_action for entity `lane` in every env (batched):
         moves int32[E][2]; returns status int32[E] (1 True, 0 False, -1 None)."""

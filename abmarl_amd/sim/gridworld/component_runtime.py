@@ -151,7 +151,7 @@ class ComponentRuntime:
             if inside:
                 in_grid.append((int(st['seq'][0, i]), aid, a))
         cells = self.grid._internal
-        if op == _abi.GW_OP_POSITION_RESET or any(cells[r, c] is not None for r in range(self.grid.rows)
+        if op in (_abi.GW_OP_POSITION_RESET, _abi.GW_OP_MAZE_RESET) or any(cells[r, c] is not None for r in range(self.grid.rows)
                          for c in range(self.grid.cols)):
             self.grid.reset()
             for _, aid, a in sorted(in_grid, key=lambda x: x[0]):

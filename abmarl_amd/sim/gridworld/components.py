@@ -71,6 +71,101 @@ class PositionState(StateBaseComponent):
             raise RuntimeError("Could not find a cell for an agent")
 
 
+class MazePlacementState(PositionState):
+    """state.py:385-619: a maze generated around the target agent
+    (generate_maze, utils.py:120-212) partitions the cells; barrier-encoded
+    agents go on its walls, free-encoded ones on its passages
+    (gw_component MAZE_RESET: maze and placement on the device)."""
+
+    def __init__(self, target_agent=None, barrier_encodings=None, free_encodings=None,
+                 cluster_barriers=False, scatter_free_agents=False, **kwargs):
+        super().__init__(**kwargs)
+        self.target_agent = target_agent
+        self.barrier_encodings = barrier_encodings
+        self.free_encodings = free_encodings
+        self.cluster_barriers = cluster_barriers
+        self.scatter_free_agents = scatter_free_agents
+
+    @property
+    def target_agent(self):
+        return self._target_agent
+
+    @target_agent.setter
+    def target_agent(self, value):
+        if type(value) is str:
+            assert value in self.agents, "The target agent must be an agent in the simulation."
+            value = self.agents[value]
+        else:
+            assert value in self.agents.values(), \
+                "The target agent must be an agent in the simulation."
+        assert isinstance(value, GridWorldAgent), "Target agent must be a GridWorld agent."
+        self._target_agent = value
+
+    @staticmethod
+    def _encoding_set(value, what):
+        if value is None:
+            return set()
+        assert type(value) is set, f"{what} encodings must be a set."
+        for encoding in value:
+            assert type(encoding) is int, f"Each {what.lower()} encoding must be an integer."
+        return value
+
+    @property
+    def barrier_encodings(self):
+        return self._barrier_encodings
+
+    @barrier_encodings.setter
+    def barrier_encodings(self, value):
+        self._barrier_encodings = self._encoding_set(value, "Barrier")
+
+    @property
+    def free_encodings(self):
+        return self._free_encodings
+
+    @free_encodings.setter
+    def free_encodings(self, value):
+        self._free_encodings = self._encoding_set(value, "Free")
+
+    @property
+    def cluster_barriers(self):
+        return self._cluster_barriers
+
+    @cluster_barriers.setter
+    def cluster_barriers(self, value):
+        assert type(value) is bool, "Cluster barriers must be a boolean."
+        self._cluster_barriers = value
+
+    @property
+    def scatter_free_agents(self):
+        return self._scatter_free_agents
+
+    @scatter_free_agents.setter
+    def scatter_free_agents(self, value):
+        assert type(value) is bool, "Scatter free agents must be a boolean."
+        self._scatter_free_agents = value
+
+    def reset(self, **kwargs):
+        """Grid.reset, the maze from the target's cell (its initial position
+        or np.random.randint(0, (rows, cols))), then every agent placed."""
+        rt = ComponentRuntime.of(self)
+        if self.randomize_placement_order:
+            items = self.__dict__.setdefault('_place_items', list(self.agents))
+            random.shuffle(items)
+            rt.eng.set_placement_order([rt.index[aid] for aid in items])
+        for agent in self.agents.values():
+            assert agent.encoding in {*self.barrier_encodings, *self.free_encodings}, \
+                "All agent encodings must be either barrier or free cell."
+        bits = lambda encs: sum(1 << int(e) for e in encs)
+        packed = (int(self.no_overlap_at_reset) | int(self.cluster_barriers) << 1 |
+                  int(self.scatter_free_agents) << 2 | rt.index[self.target_agent.id] << 8)
+        status, _, err = rt.op(_abi.GW_OP_MAZE_RESET,
+                               args=[packed, bits(self.barrier_encodings), bits(self.free_encodings)])
+        if err & _abi.GW_ERR_INIT_POSITION:
+            raise AssertionError("Cell is not available for an agent with an initial position.")
+        if err & _abi.GW_ERR_NO_CELL or not status:
+            raise RuntimeError("Could not find a cell for an agent")
+
+
 class HealthState(StateBaseComponent):
     """state.py:622-641: initial_health or np.random.uniform(0, 1)."""
 

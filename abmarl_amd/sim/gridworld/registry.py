@@ -8,7 +8,7 @@ from abmarl_amd.sim.gridworld.components import (
     SelectiveAttackActor, DoneBaseComponent, ActiveDone, OneTeamRemainingDone, TargetAgentDone,
     TargetDestroyedDone,
     ObserverBaseComponent, PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
-    StateBaseComponent, PositionState, HealthState, OrientationState,
+    StateBaseComponent, PositionState, MazePlacementState, HealthState, OrientationState,
 )
 
 _subclass_check_mapping = {
@@ -22,7 +22,7 @@ _registered_components = {
     'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor},
     'done': {ActiveDone, OneTeamRemainingDone, TargetAgentDone, TargetDestroyedDone},
     'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
-    'state': {PositionState, HealthState, OrientationState},
+    'state': {PositionState, MazePlacementState, HealthState, OrientationState},
 }
 
 registry = {

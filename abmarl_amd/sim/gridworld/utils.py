@@ -1,0 +1,49 @@
+"""generate_maze (reference: abmarl/sim/gridworld/utils.py:120-212) on the
+device: Prim's algorithm drawing from the global np.random stream, with the
+frontier in CPython's list(set(...)) order exactly as the reference
+(gw_generate_maze, csrc/gw_maze.inc).  The numpy RNG state is handed to the
+engine before the call and taken back after it, so the caller's stream
+advances by exactly the reference's draws.
+"""
+import numpy as np
+import torch
+
+from abmarl_amd import _abi
+
+_engines = {}
+
+
+def _engine(rows, cols):
+    from abmarl_amd.engine import GridWorldEngine
+    from abmarl_amd.sim.gridworld.agent import GridWorldAgent
+    from abmarl_amd.sim.gridworld.compile import agent_spec
+    eng = _engines.get((rows, cols))
+    if eng is None:
+        cc = _abi.CompiledConfig(rows, cols, [agent_spec(GridWorldAgent(id='maze', encoding=1))],
+                                 _abi.GW_SIM_TEAM_BATTLE, {}, {})
+        cc.cfg.all_lanes = 1
+        eng = _engines[(rows, cols)] = GridWorldEngine(cc, 1, seeds=[0])
+    return eng
+
+
+def generate_maze(rows, cols, start=None):
+    """A maze as a float array, 0 passage and 1 wall (utils.py:120-212)."""
+    assert type(rows) is int and rows > 0, "Rows must be a positive integer."
+    assert type(cols) is int and cols > 0, "Columns must be a positive integer."
+    if start is not None:
+        assert type(start) is np.ndarray, "Starting cell must be a numpy array."
+        assert start.shape == (2,), "Starting cell must be a 2D coordinate."
+    eng = _engine(rows, cols)
+    st = np.random.get_state()
+    assert st[0] == 'MT19937'
+    mt = np.zeros((1, _abi.GW_MT_STRIDE), np.uint32)
+    mt[0, :_abi.GW_MT_N] = st[1]
+    mt[0, _abi.GW_MT_N] = st[2]
+    eng.set_state(mt=torch.as_tensor(mt.view(np.int32), device=eng.device))
+    s = None
+    if start is not None:
+        s = torch.tensor([[int(start[0]), int(start[1])]], dtype=torch.int32, device=eng.device)
+    maze = eng.generate_maze(s)
+    out = eng.get_state()['mt'].cpu().numpy().view(np.uint32)[0]
+    np.random.set_state(('MT19937', out[:_abi.GW_MT_N].copy(), int(out[_abi.GW_MT_N])) + tuple(st[3:]))
+    return maze[0].cpu().numpy().astype(float)

@@ -348,6 +348,18 @@ gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t e
 #define GW_OP_MOVE           3
 #define GW_OP_ATTACK         4
 #define GW_OP_OBSERVE        5
+/*   GW_OP_MAZE_RESET      MazePlacementState.reset (state.py:500-619): the maze
+ *                         generated from the target's cell (generate_maze,
+ *                         utils.py:120-212, draws from the env's stream), the
+ *                         target placed there, initial-position entities, then
+ *                         barrier / free entities on maze walls / passages;
+ *                         args[e][0] = no_overlap_at_reset | cluster_barriers << 1 |
+ *                         scatter_free_agents << 2 | target lane << 8, args[e][1] =
+ *                         barrier_encodings bits, args[e][2] = free_encodings bits.
+ *                         Every entity must be a lane (gw_config.all_lanes);
+ *                         result[e][0] = 1 placed, 0 raised (err_flags:
+ *                         GW_ERR_NO_CELL / GW_ERR_INIT_POSITION).               */
+#define GW_OP_MAZE_RESET     6
 gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
                        int32_t* obs, uint32_t* err_flags, void* stream);
 
@@ -453,6 +465,14 @@ gw_status gw_set_placement_order(gw_handle h, const int32_t* lane_order, int32_t
    their cells in it.  n = 0 restores agents-dict order.  One-wave kernel,
    TeamBattle program only.                                                  */
 gw_status gw_set_action_order(gw_handle h, const int32_t* lane_order, int32_t n);
+
+/* generate_maze(rows, cols, start) (sim/gridworld/utils.py:120-212) in every
+   env, drawing from the env's np.random stream: Prim's algorithm with the
+   frontier in CPython's list(set(...)) order, exactly as the reference.
+     start  device int32[E][2] (row, col), a negative row = start None
+            (np.random.randint(1, shape - 1)); NULL = None for every env
+     maze   device int8[E][rows][cols]: 0 passage, 1 wall                     */
+gw_status gw_generate_maze(gw_handle h, const int32_t* start, int8_t* maze, void* stream);
 
 /* Introspection */
 int32_t     gw_num_envs(gw_handle h);

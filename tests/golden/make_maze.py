@@ -9,6 +9,10 @@ needs /root/reference): tests/golden/maze_gen.json.
               reset() calls after random.seed / np.random.seed: every agent's
               position, its rank inside its cell (Grid insertion order), the
               exception raised (if any) and the MT19937 state after.
+  trajectories: the reference's MultiMazeNavigationSim example
+              (examples/sim/multi_maze_navigation.py) under AllStepManager:
+              scripted moves, per step obs / reward bits / dones / positions /
+              MT19937 state, resets at __all__ or the horizon.
 """
 import json
 import os
@@ -139,14 +143,76 @@ def run_placements():
     return out
 
 
+TRAJ = [
+    dict(name='mm_10', rows=10, cols=10, navigators=3, walls=30, view=2, cluster=True, scatter=True,
+         seed=31, steps=40, horizon=20),
+    dict(name='mm_8', rows=8, cols=8, navigators=2, walls=15, view=3, cluster=False, scatter=False,
+         seed=32, steps=40, horizon=15),
+]
+
+
+def build_multi_maze(t, sim_cls, nav_cls, gw_agent_cls):
+    """The MultiMazeNavigation layout of TRAJ entry t (reference example
+    classes or this repository's)."""
+    agents = {'target': gw_agent_cls(id='target', encoding=1)}
+    for i in range(t['navigators']):
+        agents[f'navigator{i}'] = nav_cls(id=f'navigator{i}', encoding=2, view_range=t['view'])
+    for i in range(t['walls']):
+        agents[f'wall{i}'] = gw_agent_cls(id=f'wall{i}', encoding=3, blocking=True)
+    return sim_cls.build_sim(t['rows'], t['cols'], agents=agents, overlapping={1: {2}, 2: {2}},
+                             target_agent=agents['target'], barrier_encodings={3},
+                             free_encodings={1, 2}, cluster_barriers=t['cluster'],
+                             scatter_free_agents=t['scatter'])
+
+
+def multi_maze_actions(t):
+    rng = np.random.default_rng(t['seed'])
+    return rng.integers(-1, 2, size=(t['steps'], t['navigators'], 2)).tolist()
+
+
+def run_multi_maze(t, sim, manager_cls):
+    """AllStepManager episodes of sim: per step the navigators' obs, reward
+    bits, dones, every agent's position and the MT19937 state."""
+    key = 'position_centered_encoding'
+    man = manager_cls(sim)
+    np.random.seed(t['seed'])
+    navs = [f'navigator{i}' for i in range(t['navigators'])]
+    acts = multi_maze_actions(t)
+    rec = []
+    obs = man.reset()
+    ep_t = 0
+    for step in range(t['steps']):
+        entry = dict(obs={k: np.asarray(v[key]).astype(int).tolist() for k, v in obs.items()})
+        ad = {n: {'move': np.array(acts[step][i])} for i, n in enumerate(navs) if n not in man.done_agents}
+        obs, rew, done, _ = man.step(ad)
+        ep_t += 1
+        entry['reward'] = {k: np.float64(v).view(np.uint64).item() for k, v in rew.items()}
+        entry['done'] = {k: bool(v) for k, v in done.items()}
+        entry['pos'] = {k: np.asarray(a.position).astype(int).tolist() for k, a in sim.agents.items()}
+        entry['mt_pos'], entry['mt_crc'] = mt_after()
+        entry['reset'] = bool(done['__all__'] or ep_t >= t['horizon'])
+        rec.append(entry)
+        if entry['reset']:
+            obs = man.reset()
+            ep_t = 0
+    return rec
+
+
 def main():
     sys.path.insert(0, HERE)
     import gym_stub
     gym_stub.install()
     sys.path.insert(0, REF)
     from abmarl.sim.gridworld.utils import generate_maze
+    from abmarl.examples.sim.multi_maze_navigation import MultiMazeNavigationSim, MultiMazeNavigationAgent
+    from abmarl.sim.gridworld.agent import GridWorldAgent
+    from abmarl.managers import AllStepManager
+    traj = []
+    for t in TRAJ:
+        sim = build_multi_maze(t, MultiMazeNavigationSim, MultiMazeNavigationAgent, GridWorldAgent)
+        traj.append(dict(t, steps_out=run_multi_maze(t, sim, AllStepManager)))
     data = dict(python=sys.version.split()[0], numpy=np.__version__,
-                mazes=run_mazes(generate_maze), placements=run_placements())
+                mazes=run_mazes(generate_maze), placements=run_placements(), trajectories=traj)
     path = os.path.join(HERE, 'maze_gen.json')
     with open(path, 'w') as f:
         json.dump(data, f, separators=(',', ':'))
