@@ -2119,10 +2119,26 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             L.reward = 0.0;
             bool raised = false;                 // ReachTheTarget's double remove (KeyError)
 
+            // AllStepManager(randomize_action_input=True): the shuffled action
+            // dict's order (the generic kernel only; TeamBattle, ReachTheTarget,
+            // TrafficCorridor programs)
+            const int32_t* aord = (!PLAIN && p.act_order) ? p.act_order + (size_t)e * A : nullptr;
+            // body(a, k) for the lanes of m in dict order; k = the lane's rank
+            // in it (its in-cell insertion offset when it moves)
+            auto in_dict_order = [&](uint64_t m, auto&& body) {
+                if (aord) {
+                    for (int k = 0; k < A; k++) {
+                        const int a = uni(aord[k]);
+                        if ((m >> a) & 1ull) body(a, k);
+                    }
+                } else {
+                    for (uint64_t it = m; it; it &= it - 1) {
+                        const int a = first_lane(it);
+                        body(a, a);
+                    }
+                }
+            };
             if (sim_kind == GW_SIM_TEAM_BATTLE) {
-                // AllStepManager(randomize_action_input=True): the shuffled
-                // action dict's order (the generic kernel only)
-                const int32_t* aord = (!PLAIN && p.act_order) ? p.act_order + (size_t)e * A : nullptr;
                 const int my_rank = (!PLAIN && p.act_order) ? p.act_rank[(size_t)e * A + (valid ? l : 0)] : l;
                 // ---- attack pass (team_battle_example.py:35-47)
                 const bool att = acting && (L.kind & GW_K_ATTACKING) && ak > 0;
@@ -2254,14 +2270,13 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // ---- attack pass (reach_the_target.py:96-108): every acting agent,
                 // dict order; only AttackingAgents attack (others return False, [])
                 const int32_t* act_e = act_t + (size_t)e * A * p.act_dim;
-                for (uint64_t it = __ballot(acting && (L.kind & GW_K_ATTACKING)); it; it &= it - 1) {
-                    const int a = first_lane(it);
-                    if (!rlb(L.active, a)) continue;
+                in_dict_order(__ballot(acting && (L.kind & GW_K_ATTACKING)), [&](int a, int) {
+                    if (!rlb(L.active, a)) return;
                     int nlist, list;
                     const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
                         ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
                         : attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
-                    if (!status) continue;
+                    if (!status) return;
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
                         for (int t = 0; t < nlist; t++) {
@@ -2272,7 +2287,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                             }
                         }
                     }
-                }
+                });
                 STAMP(2);
                 // ---- move pass (:110-121): MovingAgents in dict order; active ones
                 // move (-0.1 on failure); then any of them on the target's cell is
@@ -2280,10 +2295,10 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // target already killed there is the reference's KeyError.
                 const int t = p.target;
                 const int tr = rl(L.r, t), tc = rl(L.c, t);         // the target never moves
-                for (uint64_t it = __ballot(acting && (L.kind & GW_K_MOVING)); it && !raised; it &= it - 1) {
-                    const int a = first_lane(it);
+                in_dict_order(__ballot(acting && (L.kind & GW_K_MOVING)), [&](int a, int k) {
+                    if (raised) return;
                     if (rlb(L.active, a)) {
-                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)k);
                         if (!ok && l == a) L.reward -= 0.1;
                     }
                     if (rl(L.r, a) == tr && rl(L.c, a) == tc) {
@@ -2293,7 +2308,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                             // reset, which the auto-reset modes do as for an ended
                             // episode (all_done set; SAME_STEP resets it right away)
                             raised = true;
-                            continue;
+                            return;
                         }
                         if (l == a) {
                             L.reward += 1.0;
@@ -2301,7 +2316,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                             L.active = false;
                         }
                     }
-                }
+                });
                 ctr += (uint32_t)WAVE;
                 if (!raised) {
                     // ---- entropy for the runners (:123-126)
@@ -2313,12 +2328,11 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // ---- traffic_corridor.py:41-49: the action dict in dict order;
                 // a failed move (None for non-MovingAgents) -0.1, then +1 when
                 // get_done(agent) holds right after the agent's own move
-                for (uint64_t it = act_mask; it; it &= it - 1) {
-                    const int a = first_lane(it);
-                    const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                in_dict_order(act_mask, [&](int a, int k) {
+                    const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)k);
                     if (!ok && l == a) L.reward -= 0.1;
                     if (lane_done_uniform(p, L, a) && l == a) L.reward += 1.0;
-                }
+                });
                 ctr += (uint32_t)WAVE;
                 build_tables(p, sm, L, true);       // the LDS table after the moves
             } else if (sim_kind == GW_SIM_MAZE_NAV) {
@@ -3397,8 +3411,11 @@ gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
     if (!g) return GW_E_INVALID;
     if (n == 0 || !lane_order) { g->base.act_order = nullptr; g->base.act_rank = nullptr; return GW_OK; }
     if (n != g->E * g->A) { set_err("action order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
-    if (g->wg || g->pacman || g->lane_envs || g->base.sim_kind != GW_SIM_TEAM_BATTLE) {
-        set_err("randomize_action_input runs with the TeamBattle program on the one-wave kernel only");
+    const int sk = g->base.sim_kind;
+    if (g->wg || g->pacman || g->lane_envs ||
+        (sk != GW_SIM_TEAM_BATTLE && sk != GW_SIM_REACH_TARGET && sk != GW_SIM_TRAFFIC)) {
+        set_err("randomize_action_input runs with the TeamBattle, ReachTheTarget and TrafficCorridor "
+                "programs on the one-wave kernel only");
         return GW_E_UNSUPPORTED;
     }
     std::vector<int32_t> both((size_t)2 * g->E * g->A);

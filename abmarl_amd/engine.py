@@ -255,13 +255,14 @@ class GridWorldEngine:
         return result
 
     def maze_reset(self, target, barrier_encodings, free_encodings, cluster_barriers=False,
-                   scatter_free_agents=False, no_overlap_at_reset=False, result=None):
-        """MazePlacementState.reset (state.py:500-619) in every env
+                   scatter_free_agents=False, no_overlap_at_reset=False, result=None, maze=True):
+        """MazePlacementState.reset (state.py:500-619) in every env, or with
+        maze=False TargetBarriersFreePlacementState.reset (state.py:279-382)
         (gw_component GW_OP_MAZE_RESET); returns status int32[E] (1 placed)."""
         bits = lambda encs: sum(1 << int(x) for x in encs)
         args = torch.zeros((self.E, self.act_dim), dtype=torch.int32, device=self.device)
         args[:, 0] = (int(bool(no_overlap_at_reset)) | int(bool(cluster_barriers)) << 1 |
-                      int(bool(scatter_free_agents)) << 2 | int(target) << 8)
+                      int(bool(scatter_free_agents)) << 2 | int(not maze) << 3 | int(target) << 8)
         args[:, 1] = bits(barrier_encodings)
         args[:, 2] = bits(free_encodings)
         res = result if result is not None else \

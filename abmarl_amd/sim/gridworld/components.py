@@ -71,11 +71,11 @@ class PositionState(StateBaseComponent):
             raise RuntimeError("Could not find a cell for an agent")
 
 
-class MazePlacementState(PositionState):
-    """state.py:385-619: a maze generated around the target agent
-    (generate_maze, utils.py:120-212) partitions the cells; barrier-encoded
-    agents go on its walls, free-encoded ones on its passages
-    (gw_component MAZE_RESET: maze and placement on the device)."""
+class _TargetPlacementState(PositionState):
+    """The constructor, properties and reset shared by the two target-relative
+    placements (state.py:169-382, 385-619); _maze selects the variant."""
+
+    _maze = False
 
     def __init__(self, target_agent=None, barrier_encodings=None, free_encodings=None,
                  cluster_barriers=False, scatter_free_agents=False, **kwargs):
@@ -157,13 +157,32 @@ class MazePlacementState(PositionState):
                 "All agent encodings must be either barrier or free cell."
         bits = lambda encs: sum(1 << int(e) for e in encs)
         packed = (int(self.no_overlap_at_reset) | int(self.cluster_barriers) << 1 |
-                  int(self.scatter_free_agents) << 2 | rt.index[self.target_agent.id] << 8)
+                  int(self.scatter_free_agents) << 2 | int(not self._maze) << 3 |
+                  rt.index[self.target_agent.id] << 8)
         status, _, err = rt.op(_abi.GW_OP_MAZE_RESET,
                                args=[packed, bits(self.barrier_encodings), bits(self.free_encodings)])
         if err & _abi.GW_ERR_INIT_POSITION:
             raise AssertionError("Cell is not available for an agent with an initial position.")
         if err & _abi.GW_ERR_NO_CELL or not status:
             raise RuntimeError("Could not find a cell for an agent")
+
+
+class TargetBarriersFreePlacementState(_TargetPlacementState):
+    """state.py:169-382: the target placed first (its initial position or
+    np.random.randint(0, (rows, cols))); barrier agents clustered near it,
+    free agents scattered away from it (gw_component MAZE_RESET, variant 1:
+    no maze, every cell available to both kinds)."""
+
+    _maze = False
+
+
+class MazePlacementState(_TargetPlacementState):
+    """state.py:385-619: a maze generated around the target agent
+    (generate_maze, utils.py:120-212) partitions the cells; barrier-encoded
+    agents go on its walls, free-encoded ones on its passages
+    (gw_component MAZE_RESET: maze and placement on the device)."""
+
+    _maze = True
 
 
 class HealthState(StateBaseComponent):

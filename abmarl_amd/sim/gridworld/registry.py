@@ -8,7 +8,8 @@ from abmarl_amd.sim.gridworld.components import (
     SelectiveAttackActor, DoneBaseComponent, ActiveDone, OneTeamRemainingDone, TargetAgentDone,
     TargetDestroyedDone,
     ObserverBaseComponent, PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
-    StateBaseComponent, PositionState, MazePlacementState, HealthState, OrientationState,
+    StateBaseComponent, PositionState, MazePlacementState, TargetBarriersFreePlacementState,
+    HealthState, OrientationState,
 )
 
 _subclass_check_mapping = {
@@ -22,7 +23,8 @@ _registered_components = {
     'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor},
     'done': {ActiveDone, OneTeamRemainingDone, TargetAgentDone, TargetDestroyedDone},
     'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
-    'state': {PositionState, MazePlacementState, HealthState, OrientationState},
+    'state': {PositionState, MazePlacementState, TargetBarriersFreePlacementState, HealthState,
+              OrientationState},
 }
 
 registry = {

@@ -175,10 +175,11 @@ class DictRuntime:
         ids = [a for a in action_dict]
         order = [self.index[a] for a in ids]
         shuffled = order != sorted(order)
-        if shuffled and (self.lazy or self.cc.cfg.sim_kind != _abi.GW_SIM_TEAM_BATTLE):
+        if shuffled and (self.lazy or self.cc.cfg.sim_kind not in (
+                _abi.GW_SIM_TEAM_BATTLE, _abi.GW_SIM_REACH_TARGET, _abi.GW_SIM_TRAFFIC)):
             raise NotImplementedError(
                 "an action dict in another order than the agents dict (randomize_action_input) "
-                "runs with the TeamBattle program only")
+                "runs with the TeamBattle, ReachTheTarget and TrafficCorridor programs only")
         if self.lazy:
             return self._lazy_step(action_dict)
         # AllStepManager(randomize_action_input=True): the shuffled dict's order

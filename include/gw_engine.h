@@ -354,8 +354,11 @@ gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t e
  *                         target placed there, initial-position entities, then
  *                         barrier / free entities on maze walls / passages;
  *                         args[e][0] = no_overlap_at_reset | cluster_barriers << 1 |
- *                         scatter_free_agents << 2 | target lane << 8, args[e][1] =
- *                         barrier_encodings bits, args[e][2] = free_encodings bits.
+ *                         scatter_free_agents << 2 | variant << 3 | target lane << 8,
+ *                         args[e][1] = barrier_encodings bits, args[e][2] =
+ *                         free_encodings bits.  variant 1 =
+ *                         TargetBarriersFreePlacementState.reset (state.py:279-382):
+ *                         no maze, every cell available to both kinds.
  *                         Every entity must be a lane (gw_config.all_lanes);
  *                         result[e][0] = 1 placed, 0 raised (err_flags:
  *                         GW_ERR_NO_CELL / GW_ERR_INIT_POSITION).               */
@@ -460,10 +463,11 @@ gw_status gw_set_placement_order(gw_handle h, const int32_t* lane_order, int32_t
 /* AllStepManager(randomize_action_input=True) (all_step_manager.py:62-65):
    the order of the action dict the next steps process, lane_order[E][A]
    (host memory; per env a permutation of 0..A-1: the lanes in the shuffled
-   dict first, the others after).  The TeamBattle program's attack and move
-   passes go in that order (team_battle_example.py:33-59) and movers enter
-   their cells in it.  n = 0 restores agents-dict order.  One-wave kernel,
-   TeamBattle program only.                                                  */
+   dict first, the others after).  The attack and move passes of the
+   TeamBattle (team_battle_example.py:33-59) and ReachTheTarget
+   (reach_the_target.py:95-126) programs and the TrafficCorridor moves
+   (traffic_corridor.py:41-49) go in that order, and movers enter their cells
+   in it.  n = 0 restores agents-dict order.  One-wave kernel only.          */
 gw_status gw_set_action_order(gw_handle h, const int32_t* lane_order, int32_t n);
 
 /* generate_maze(rows, cols, start) (sim/gridworld/utils.py:120-212) in every

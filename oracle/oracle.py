@@ -63,7 +63,7 @@ def lib():
         L.gwo_pyset_order.argtypes = [vp, C.c_int32, C.c_int32, vp]
         L.gwo_maze_place.restype = C.c_uint32
         L.gwo_maze_place.argtypes = [vp, C.c_int32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32,
-                                     C.c_int32, vp, vp, vp, vp, vp, vp]
+                                     C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32]
         _lib = L
     return _lib
 
@@ -201,8 +201,9 @@ def generate_maze(rows, cols, start, mt):
 
 
 def maze_place(compiled, target, barrier, free, mt, cluster=False, scatter=False,
-               no_overlap=False, order=None):
-    """MazePlacementState.reset (state.py:500-619) of every entity of compiled."""
+               no_overlap=False, order=None, variant=0):
+    """MazePlacementState.reset (state.py:500-619) of every entity of compiled;
+    variant 1: TargetBarriersFreePlacementState.reset (state.py:279-382)."""
     n = compiled.n_agents
     bits = lambda encs: sum(1 << int(e) for e in encs)
     pos = np.zeros((n, 2), np.int32)
@@ -212,7 +213,7 @@ def maze_place(compiled, target, barrier, free, mt, cluster=False, scatter=False
     o = None if order is None else np.ascontiguousarray(order, np.int32)
     err = lib().gwo_maze_place(C.cast(C.byref(compiled.cfg), C.c_void_p), int(target), bits(barrier),
                                bits(free), int(cluster), int(scatter), int(no_overlap), _p(o), _p(mt),
-                               _p(pos), _p(seq), _p(in_grid), _p(maze))
+                               _p(pos), _p(seq), _p(in_grid), _p(maze), int(variant))
     return dict(err=int(err), pos=pos, seq=seq, in_grid=in_grid, maze=maze)
 
 

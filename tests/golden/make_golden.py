@@ -150,6 +150,16 @@ CASES = [
          overlap={1: [1, 2], 2: [2, 1]},
          agent=dict(move_range=1, attack_range=1, attack_strength=0.6, attack_accuracy=0.7,
                     view_range=2)),
+    # the same for the ReachTheTarget and TrafficCorridor programs: runners move
+    # (and enter cells) in the shuffled dict's order
+    dict(name='rtt_shuffle_act', kind='rtt', rows=9, cols=9, n_barriers=12, n_runners=24, n_envs=4,
+         n_steps=120, horizon=40, seed_base=61, randomize_action_input=True,
+         runner=dict(move_range=1, view_range=2),
+         target=dict(view_range=2, attack_range=1, attack_strength=0.6, attack_accuracy=0.8,
+                     simultaneous_attacks=2)),
+    dict(name='traffic_shuffle_act', kind='traffic', n_envs=4, n_steps=150, horizon=60, seed_base=63,
+         randomize_action_input=True,
+         grid=['G_WWWWW_R', 'G_______R', 'r___W___g', 'G_______R', 'G_WWWWW_R'], targets='team'),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
@@ -178,6 +188,8 @@ def maze_array(spec):
 
 def full_case(case):
     c = dict(case)
+    if c.get('kind') in ('traffic', 'rtt') and c.get('randomize_action_input', False):
+        c['py_seeds'] = [(c['seed_base'] * 7919 + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
     if c.get('kind') == 'traffic':
         c['seeds'] = [(c['seed_base'] + e) & 0xFFFFFFFF for e in range(c['n_envs'])]
         c['action_seed'] = 1234 + c['seed_base']
@@ -279,7 +291,7 @@ def build_reference_rtt(c):
     agents['target'] = TargetAgent(**kw)
     sim = ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
                                       attack_mapping={2: {3}})
-    return AllStepManager(sim)
+    return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
 def traffic_registry(TrafficAgent, TargetAgent, WallAgent):
@@ -313,7 +325,7 @@ def build_reference_traffic(c):
     sim = TrafficCorridorSimulation.build_sim_from_array(
         arr, reg, overlapping={1: {1}, 2: {2}}, states={'PositionState'}, dones={'TargetAgentDone'},
         observers={'PositionCenteredEncodingObserver'}, target_mapping=mapping)
-    return AllStepManager(sim)
+    return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
 def build_reference_env(c):

@@ -83,6 +83,16 @@ PLACEMENTS = [
 ]
 
 
+# TargetBarriersFreePlacementState (state.py:169-382): the same case shapes
+TBF = [dict(c, name='tbf_' + c['name']) for c in PLACEMENTS
+       if c['name'] in ('basic', 'target_ip', 'cluster_scatter', 'cluster_scatter_no_overlap',
+                        'cluster_only', 'scatter_only', 'ip_agents', 'ip_conflict', 'both_sets',
+                        'shuffled', 'multi_maze')]
+TBF.append(dict(name='tbf_too_many', rows=3, cols=3,
+                agents=[('target', 1, None)] + [(f'b{i}', 2, None) for i in range(10)],
+                overlapping={}, barrier=[2], free=[1], cluster=True, seed=40, resets=2))
+
+
 def mt_after():
     st = np.random.get_state()
     return int(st[2]), int(zlib.crc32(np.asarray(st[1], np.uint32).tobytes()))
@@ -99,12 +109,13 @@ def run_mazes(generate_maze):
     return out
 
 
-def run_placements():
+def run_placements(cases=None, cls_name='MazePlacementState'):
     from abmarl.sim.gridworld.grid import Grid
     from abmarl.sim.gridworld.agent import GridWorldAgent
-    from abmarl.sim.gridworld.state import MazePlacementState
+    from abmarl.sim.gridworld import state as ref_state
+    MazePlacementState = getattr(ref_state, cls_name)
     out = []
-    for c in PLACEMENTS:
+    for c in (PLACEMENTS if cases is None else cases):
         agents = {aid: GridWorldAgent(id=aid, encoding=enc,
                                       initial_position=None if ip is None else np.array(ip))
                   for aid, enc, ip in c['agents']}
@@ -212,7 +223,8 @@ def main():
         sim = build_multi_maze(t, MultiMazeNavigationSim, MultiMazeNavigationAgent, GridWorldAgent)
         traj.append(dict(t, steps_out=run_multi_maze(t, sim, AllStepManager)))
     data = dict(python=sys.version.split()[0], numpy=np.__version__,
-                mazes=run_mazes(generate_maze), placements=run_placements(), trajectories=traj)
+                mazes=run_mazes(generate_maze), placements=run_placements(), trajectories=traj,
+                tbf=run_placements(TBF, 'TargetBarriersFreePlacementState'))
     path = os.path.join(HERE, 'maze_gen.json')
     with open(path, 'w') as f:
         json.dump(data, f, separators=(',', ':'))

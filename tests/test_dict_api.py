@@ -36,7 +36,8 @@ def _action(agent, a):
 
 @pytest.mark.parametrize('name', ['tb_small', 'tb_mixed', 'tb_order', 'tb_corners', 'tb_walls',
                                   'maze_file', 'maze_16', 'rtt_7', 'rtt_16', 'rtt_double',
-                                  'tb_shuffle', 'tb_shuffle_act'])
+                                  'tb_shuffle', 'tb_shuffle_act', 'rtt_shuffle_act',
+                                  'traffic_shuffle_act'])
 def test_dict_api_matches_reference(name):
     g = load_golden(name)
     c = g['case']

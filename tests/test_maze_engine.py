@@ -76,13 +76,16 @@ def test_generate_maze_vs_oracle_batched(rows, cols, E):
 
 
 @gpu
-@pytest.mark.parametrize('name', [c['name'] for c in DATA['placements']])
+@pytest.mark.parametrize('name', [c['name'] for c in DATA['placements']] + [c['name'] for c in DATA['tbf']])
 def test_maze_placement_state_reference(name):
-    """The reference's MazePlacementState resets through the component API
-    (MazePlacementState.reset -> gw_component MAZE_RESET): positions, in-cell
-    order, the exception raised and the numpy MT19937 state after each."""
-    from abmarl_amd.sim.gridworld.components import MazePlacementState
-    case = next(c for c in DATA['placements'] if c['name'] == name)
+    """The reference's MazePlacementState (and, tbf_*, TargetBarriersFree-
+    PlacementState) resets through the component API (reset -> gw_component
+    MAZE_RESET): positions, in-cell order, the exception raised and the
+    numpy MT19937 state after each."""
+    from abmarl_amd.sim.gridworld.components import MazePlacementState, TargetBarriersFreePlacementState
+    if name.startswith('tbf_'):
+        MazePlacementState = TargetBarriersFreePlacementState  # noqa: N806
+    case = next(c for c in DATA['placements'] + DATA['tbf'] if c['name'] == name)
     agents, grid, _ = mc.build(case)
     ids = list(agents)
     state = MazePlacementState(
@@ -146,13 +149,15 @@ def test_maze_placement_known_answers():
 
 
 @gpu
-@pytest.mark.parametrize('name', ['multi_maze', 'cluster_scatter', 'scatter_only', 'both_sets', 'too_many'])
+@pytest.mark.parametrize('name', ['multi_maze', 'cluster_scatter', 'scatter_only', 'both_sets', 'too_many',
+                                  'tbf_multi_maze', 'tbf_cluster_scatter', 'tbf_basic', 'tbf_too_many'])
 def test_maze_reset_batched_vs_oracle(name):
     """Batched MazePlacementState.reset (engine.maze_reset) at 512 envs, each
     on its own stream, three consecutive resets, env by env against the
     oracle: positions, placement order, error flags, MT19937 state."""
     from oracle import oracle
-    case = next(c for c in DATA['placements'] if c['name'] == name)
+    case = next(c for c in DATA['placements'] + DATA['tbf'] if c['name'] == name)
+    variant = int(name.startswith('tbf_'))
     _, _, cc = mc.build(case)
     E = 512
     ids = [a[0] for a in case['agents']]
@@ -162,11 +167,12 @@ def test_maze_reset_batched_vs_oracle(name):
     eng.set_state(mt=torch.as_tensor(_mt_rows(seeds).view(np.int32), device=eng.device))
     mts = [oracle.mt_state(int(s)) for s in seeds]
     kw = dict(cluster=case.get('cluster', False), scatter=case.get('scatter', False),
-              no_overlap=case.get('no_overlap', False))
+              no_overlap=case.get('no_overlap', False), variant=variant)
     for _ in range(3):
         eng.err.zero_()
         status = eng.maze_reset(tgt, case['barrier'], case['free'], cluster_barriers=kw['cluster'],
-                                scatter_free_agents=kw['scatter'], no_overlap_at_reset=kw['no_overlap'])
+                                scatter_free_agents=kw['scatter'], no_overlap_at_reset=kw['no_overlap'],
+                                maze=not variant)
         st = {k: v.cpu().numpy() for k, v in eng.get_state().items()}
         err = eng.err.cpu().numpy()
         status = status.cpu().numpy()

@@ -58,3 +58,22 @@ def test_set_order_rule_vs_python():
         cells = rng.permutation(rows * cols)[:n]
         want = [r * cols + c for r, c in list(set((int(x) // cols, int(x) % cols) for x in cells))]
         assert oracle.pyset_order(cells, cols) == want
+
+
+@pytest.mark.parametrize('name', [c['name'] for c in DATA['tbf']])
+def test_target_barriers_free_placement_matches_reference(name):
+    """TargetBarriersFreePlacementState (state.py:169-382): the oracle's
+    variant 1 against the reference's resets."""
+    case = next(c for c in DATA['tbf'] if c['name'] == name)
+    agents, grid, cc = mc.build(case)
+    ids = list(agents)
+    mt = oracle.mt_state(case['seed'])
+    for rec in case['resets_out']:
+        order = None if rec['order'] is None else [ids.index(a) for a in rec['order']]
+        out = oracle.maze_place(cc, ids.index('target'), case['barrier'], case['free'], mt,
+                                cluster=case.get('cluster', False), scatter=case.get('scatter', False),
+                                no_overlap=case.get('no_overlap', False), order=order, variant=1)
+        assert mc.RAISED[out['err']] == rec['raised']
+        if rec['raised'] is None:
+            assert mc.cells_of(out['pos'], out['seq'], out['in_grid']) == rec['cells']
+        assert int(mt[624]) == rec['mt_pos'] and mc.mt_key_crc(mt) == rec['mt_crc']

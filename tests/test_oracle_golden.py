@@ -61,12 +61,13 @@ def test_shuffle_fixture_needs_the_shuffle(oracle_mod):
     assert json.loads(json.dumps(g['case']))['randomize_placement_order'] is True
 
 
-def test_shuffled_action_fixture_needs_the_shuffle(oracle_mod):
-    """tb_shuffle_act (AllStepManager(randomize_action_input=True), replayed
-    on the GPU through the dict API by test_dict_api.py) is evidence only if
-    the shuffled action order changes the trajectory: the agents-dict order
-    from the same seeds and actions diverges from it."""
-    g = load_golden('tb_shuffle_act')
+@pytest.mark.parametrize('name', ['tb_shuffle_act', 'rtt_shuffle_act', 'traffic_shuffle_act'])
+def test_shuffled_action_fixture_needs_the_shuffle(oracle_mod, name):
+    """The *_shuffle_act fixtures (AllStepManager(randomize_action_input=True),
+    replayed on the GPU through the dict API by test_dict_api.py) are evidence
+    only if the shuffled action order changes the trajectory: the agents-dict
+    order from the same seeds and actions diverges from it."""
+    g = load_golden(name)
     assert g['case']['randomize_action_input'] is True
     with pytest.raises(AssertionError):
         replay(OracleRunner(oracle_mod, g), g)
