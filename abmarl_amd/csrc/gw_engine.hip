@@ -3412,10 +3412,11 @@ gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
     if (n == 0 || !lane_order) { g->base.act_order = nullptr; g->base.act_rank = nullptr; return GW_OK; }
     if (n != g->E * g->A) { set_err("action order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
     const int sk = g->base.sim_kind;
-    if (g->wg || g->pacman || g->lane_envs ||
-        (sk != GW_SIM_TEAM_BATTLE && sk != GW_SIM_REACH_TARGET && sk != GW_SIM_TRAFFIC)) {
-        set_err("randomize_action_input runs with the TeamBattle, ReachTheTarget and TrafficCorridor "
-                "programs on the one-wave kernel only");
+    if (g->lane_envs || (g->wg && sk != GW_SIM_REACH_TARGET) ||
+        (sk != GW_SIM_TEAM_BATTLE && sk != GW_SIM_REACH_TARGET && sk != GW_SIM_TRAFFIC &&
+         sk != GW_SIM_PACMAN)) {
+        set_err("randomize_action_input runs with the TeamBattle, ReachTheTarget, TrafficCorridor "
+                "and Pacman programs (the workgroup-per-env kernel: ReachTheTarget only)");
         return GW_E_UNSUPPORTED;
     }
     std::vector<int32_t> both((size_t)2 * g->E * g->A);

@@ -175,13 +175,12 @@ class DictRuntime:
         ids = [a for a in action_dict]
         order = [self.index[a] for a in ids]
         shuffled = order != sorted(order)
-        if shuffled and (self.lazy or self.cc.cfg.sim_kind not in (
-                _abi.GW_SIM_TEAM_BATTLE, _abi.GW_SIM_REACH_TARGET, _abi.GW_SIM_TRAFFIC)):
+        if shuffled and self.cc.cfg.sim_kind not in (
+                _abi.GW_SIM_TEAM_BATTLE, _abi.GW_SIM_REACH_TARGET, _abi.GW_SIM_TRAFFIC,
+                _abi.GW_SIM_PACMAN):
             raise NotImplementedError(
                 "an action dict in another order than the agents dict (randomize_action_input) "
-                "runs with the TeamBattle, ReachTheTarget and TrafficCorridor programs only")
-        if self.lazy:
-            return self._lazy_step(action_dict)
+                "runs with the TeamBattle, ReachTheTarget, TrafficCorridor and Pacman programs only")
         # AllStepManager(randomize_action_input=True): the shuffled dict's order
         if shuffled:
             first = [int(self.lane_of[i]) for i in order if self.lane_of[i] >= 0]
@@ -191,6 +190,8 @@ class DictRuntime:
         elif getattr(self, '_act_order_set', False):
             self.eng.set_action_order(None)
             self._act_order_set = False
+        if self.lazy:
+            return self._lazy_step(action_dict)
         act = np.zeros((1, len(self.lanes), self.eng.act_dim), np.int32)
         act[0, :, 2] = -1                      # not in action_dict: does not act
         for aid, a in action_dict.items():

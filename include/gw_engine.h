@@ -466,8 +466,9 @@ gw_status gw_set_placement_order(gw_handle h, const int32_t* lane_order, int32_t
    dict first, the others after).  The attack and move passes of the
    TeamBattle (team_battle_example.py:33-59) and ReachTheTarget
    (reach_the_target.py:95-126) programs and the TrafficCorridor moves
-   (traffic_corridor.py:41-49) go in that order, and movers enter their cells
-   in it.  n = 0 restores agents-dict order.  One-wave kernel only.          */
+   (traffic_corridor.py:41-49) and the Pacman program's baddie moves
+   (pacman.py:104-117) go in that order, and movers enter their cells in it.
+   n = 0 restores agents-dict order.  One-wave kernels only.                 */
 gw_status gw_set_action_order(gw_handle h, const int32_t* lane_order, int32_t n);
 
 /* generate_maze(rows, cols, start) (sim/gridworld/utils.py:120-212) in every

@@ -35,6 +35,11 @@ CASES = [
     # the full pacman.txt (ten baddies), examples/rllib_pacman.py's scheme + kill
     dict(name='pacman_10', baddies=None, n_envs=4, n_steps=120, horizon=80, seed_base=777,
          reward_scheme={'bad_move': 0, 'entropy': -0.01, 'eat_food': 0.05, 'kill': 1, 'die': -1}),
+    # AllStepManager(randomize_action_input=True): the baddies move in the
+    # shuffled action dict's order (Python's random, per env)
+    dict(name='pacman_shuffle_act', baddies=None, n_envs=4, n_steps=120, horizon=80, seed_base=881,
+         reward_scheme={'bad_move': -0.1, 'entropy': -0.01, 'eat_food': 0.05, 'kill': 1, 'die': -1},
+         randomize_action_input=True),
 ]
 
 
@@ -61,7 +66,7 @@ def build_reference(c):
     ori = [s for s in sim._states if isinstance(s, OrientationState)][0]
     hea = [s for s in sim._states if isinstance(s, HealthState)][0]
     sim._states = [pos, ori, hea]
-    return AllStepManager(sim), FoodAgent
+    return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False)), FoodAgent
 
 
 def run_case(c):
@@ -94,11 +99,17 @@ def run_case(c):
         food = np.array([ag[i].active for i in food_ix], dtype=np.uint8)
         return pos, ori, food, float(m.sim.pacman.health)
 
-    rng_states, obs0 = [], np.zeros((E, NA, H, W), np.int8)
+    import random
+    if c.get('randomize_action_input'):
+        c['py_seeds'] = [(c['seed_base'] * 7919 + e) & 0xFFFFFFFF for e in range(E)]
+    rng_states, py_states, obs0 = [], [], np.zeros((E, NA, H, W), np.int8)
     for e in range(E):
         np.random.seed(c['seeds'][e])
+        if 'py_seeds' in c:
+            random.seed(c['py_seeds'][e])
         obs0[e], _ = obs_array(managers[e].reset())
         rng_states.append(np.random.get_state())
+        py_states.append(random.getstate())
     out = dict(
         obs=np.full((T, E, NA, H, W), -2, dtype=np.int8),
         returned=np.zeros((T, E, NA), np.uint8),
@@ -119,6 +130,7 @@ def run_case(c):
         for e in range(E):
             m = managers[e]
             np.random.set_state(rng_states[e])
+            random.setstate(py_states[e])
             adict = {ids[i]: {'move': int(act[t, e, j])} for j, i in enumerate(agents_ix)
                      if ids[i] not in m.done_agents}
             o, r, d, _ = m.step(adict)
@@ -140,6 +152,7 @@ def run_case(c):
                 out['reset_mask'][t, e] = 1
                 out['reset_obs'][t, e], _ = obs_array(ro)
             rng_states[e] = np.random.get_state()
+            py_states[e] = random.getstate()
     path = os.path.join(HERE, c['name'] + '.npz')
     np.savez_compressed(path, case=json.dumps(c), actions=act, obs0=obs0, **out)
     deaths = int(((out['pac_health'] == 0) & (out['all_done'] == 1)).sum())

@@ -131,3 +131,64 @@ def test_engine_workgroup_team_battle_matches_reference(name):
     r = EngineRunner(g, force_workgroup=True)
     assert r.eng.wg
     replay(r, g)
+
+
+class ShuffledOrderRunner(EngineRunner):
+    """EngineRunner for the *_shuffle_act fixtures (AllStepManager(
+    randomize_action_input=True)): before every step, each env's action dict
+    -- its live Agents in agents-dict order -- is shuffled with that env's
+    Python random stream exactly as all_step_manager.py:62-65 (seeded from
+    the fixture's py_seeds before the first reset), and the batch of orders
+    goes to the engine (gw_set_action_order)."""
+
+    def __init__(self, g, force_workgroup=False):
+        import random
+        super().__init__(g, force_workgroup)
+        c = g['case']
+        self.py = []
+        for e in range(self.E):
+            random.seed(c['py_seeds'][e])
+            self.py.append(random.getstate())
+        from abmarl_amd import _abi
+        k = np.array([sp.kind for sp in self.cc.specs])
+        self.is_agent = ((k & _abi.GW_K_OBSERVING) != 0) & ((k & _abi.GW_K_ACTING) != 0)
+        self.lane_of = np.full(self.NE, -1)
+        self.lane_of[self.lanes] = np.arange(len(self.lanes))
+        self.dead = [set() for _ in range(self.E)]
+
+    def reset(self, mask):
+        for e in range(self.E):
+            if mask is None or mask[e]:
+                self.dead[e] = set()
+        return super().reset(mask)
+
+    def step(self, actions):
+        import random
+        orders = []
+        for e in range(self.E):
+            live = [i for i in range(self.NE) if self.is_agent[i] and i not in self.dead[e]]
+            random.setstate(self.py[e])
+            random.shuffle(live)
+            self.py[e] = random.getstate()
+            first = [int(self.lane_of[i]) for i in live]
+            orders.append(first + [k for k in range(len(self.lanes)) if k not in set(first)])
+        self.eng.set_action_order(np.array(orders, np.int32))
+        obs, rew, done, ad = super().step(actions)
+        err = self.errors()
+        for e in range(self.E):
+            if not (err[e] & 4):
+                self.dead[e] |= {i for i in range(self.NE) if self.is_agent[i] and done[e, i]}
+        return obs, rew, done, ad
+
+
+@pytest.mark.parametrize('name,force_workgroup', [
+    ('tb_shuffle_act', False), ('rtt_shuffle_act', False), ('rtt_shuffle_act', True),
+    ('traffic_shuffle_act', False)])
+def test_engine_shuffled_action_order_matches_reference(name, force_workgroup):
+    """Batched gw_set_action_order (every env its own shuffled order each
+    step) on the one-wave kernel and, for ReachTheTarget, the workgroup-per-env
+    kernel, against the reference's own shuffled trajectories."""
+    g = load_golden(name)
+    r = ShuffledOrderRunner(g, force_workgroup=force_workgroup)
+    assert r.eng.wg == force_workgroup
+    replay(r, g)

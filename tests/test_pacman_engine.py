@@ -76,17 +76,23 @@ def test_batched_allstep_matches_reference(name):
             assert (o[rs.astype(bool)] == g['reset_obs'][t][rs.astype(bool)]).all(), f"step {t}: reset"
 
 
-def test_dict_allstep_matches_reference():
-    """build_pacman + AllStepManager, np.random.seed per env, as the reference."""
+@pytest.mark.parametrize('name', ['pacman_4', 'pacman_shuffle_act'])
+def test_dict_allstep_matches_reference(name):
+    """build_pacman + AllStepManager, np.random.seed per env, as the reference;
+    pacman_shuffle_act: AllStepManager(randomize_action_input=True), the
+    baddies moving in the shuffled dict's order (Python's random per env)."""
+    import random
     from abmarl_amd.managers import AllStepManager
-    g = load('pacman_4')
+    g = load(name)
     c = g['case']
     for e in range(2):
         sim = _sim(c)
         ids = list(sim.agents)
         agents = [ids[i] for i in c['agent_index']]
-        m = AllStepManager(sim)
+        m = AllStepManager(sim, randomize_action_input=bool(c.get('randomize_action_input', False)))
         np.random.seed(c['seeds'][e])
+        if 'py_seeds' in c:
+            random.seed(c['py_seeds'][e])
         o = m.reset()
         for j, aid in enumerate(agents):
             assert (o[aid]['absolute_encoding'] == g['obs0'][e, j]).all()

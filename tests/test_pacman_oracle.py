@@ -70,6 +70,16 @@ def test_oracle_matches_reference(oracle_mod, name):
                 assert (obs[e, ag] == g['reset_obs'][t, e]).all(), f"step {t} env {e}: reset obs"
 
 
+def test_shuffled_pacman_is_order_invariant(oracle_mod):
+    """pacman_shuffle_act (AllStepManager(randomize_action_input=True), the
+    reference's own trajectory) replays in agents-dict order too: every
+    baddie has encoding 4 and overlaps the others, so the order they move and
+    stack in changes no observation, draw or reward bit.  The GPU replay
+    (test_pacman_engine.py) still runs the shuffled order, which only has to
+    leave the Python and numpy streams where the reference leaves them."""
+    test_oracle_matches_reference(oracle_mod, 'pacman_shuffle_act')
+
+
 class _OracleSim:
     """The oracle's simulation-only protocol (gwo_sim_*, gwo_observe,
     gwo_take_reward) behind the AgentBasedSimulation calls a manager makes,
