@@ -3718,13 +3718,11 @@ static gw_status maze_launch(gw_engine* g, int mode, const int32_t* args, const 
     m.mode = mode; m.start = start; m.maze_out = maze;
     m.T = maze_table_slots(g->H, g->W);
     const size_t smem = maze_smem_bytes(g->H, g->W, m.T);
-    static bool attr_set = false;
-    if (!attr_set) {
-        HIPCHK(hipFuncSetAttribute((const void*)maze_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024));
-        attr_set = true;
-    }
     if (smem > 160 * 1024) { set_err("maze: %zu B of LDS per env", smem); return GW_E_UNSUPPORTED; }
+    // per call: the attribute belongs to the current device
+    if (smem > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)maze_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)smem));
     Params p = g->base;
     p.actions = args; p.comp_out = result; p.err = err_flags;
     hipLaunchKernelGGL(maze_kernel, dim3(g->E), dim3(WAVE), smem, st, p, m);
