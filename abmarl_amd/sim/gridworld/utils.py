@@ -33,6 +33,14 @@ def generate_maze(rows, cols, start=None):
     if start is not None:
         assert type(start) is np.ndarray, "Starting cell must be a numpy array."
         assert start.shape == (2,), "Starting cell must be a 2D coordinate."
+        r, c = int(start[0]), int(start[1])
+        if not (-(rows + 2) <= r + 1 < rows + 2 and -(cols + 2) <= c + 1 < cols + 2):
+            # the reference's grid[tuple(start + 1)] = 0 on the bordered grid
+            raise IndexError(f"index {[r + 1, c + 1]} is out of bounds for the bordered "
+                             f"{rows + 2}x{cols + 2} maze grid")
+        if not (0 <= r < rows and 0 <= c < cols):
+            raise NotImplementedError("a start outside the maze (numpy's wrapped / border index) "
+                                      "is not supported on the device")
     eng = _engine(rows, cols)
     st = np.random.get_state()
     assert st[0] == 'MT19937'

@@ -475,7 +475,9 @@ gw_status gw_set_action_order(gw_handle h, const int32_t* lane_order, int32_t n)
    env, drawing from the env's np.random stream: Prim's algorithm with the
    frontier in CPython's list(set(...)) order, exactly as the reference.
      start  device int32[E][2] (row, col), a negative row = start None
-            (np.random.randint(1, shape - 1)); NULL = None for every env
+            (np.random.randint(1, shape - 1)); NULL = None for every env;
+            a start outside the maze leaves the env's stream untouched and
+            its maze all -1
      maze   device int8[E][rows][cols]: 0 passage, 1 wall                     */
 gw_status gw_generate_maze(gw_handle h, const int32_t* start, int8_t* maze, void* stream);
 

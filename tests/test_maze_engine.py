@@ -263,3 +263,35 @@ def test_multi_maze_navigation_replays_reference(k):
         assert int(st[2]) == want['mt_pos'] and mc.mt_key_crc(np.asarray(st[1], np.uint32)) == want['mt_crc'], where
         if want['reset']:
             obs = man.reset()
+
+
+def test_generate_maze_utility_validation():
+    """tests/sim/gridworld/test_utils.py:18-31 (reference): argument checks
+    (raised on the host, before any device work)."""
+    from abmarl_amd.sim.gridworld.utils import generate_maze
+    with pytest.raises(AssertionError):
+        generate_maze(0, 4)
+    with pytest.raises(AssertionError):
+        generate_maze(3, -1)
+    with pytest.raises(AssertionError):
+        generate_maze(3, 3, [0, 1])
+    with pytest.raises(AssertionError):
+        generate_maze(3, 3, np.array([0]))
+    with pytest.raises(IndexError):
+        generate_maze(3, 3, np.array([6, 13]))
+
+
+@gpu
+def test_generate_maze_bad_start_on_device():
+    """A start outside the maze through the C-ABI: that env's maze is all -1
+    and its stream is untouched; the other envs are unaffected."""
+    eng = _engine(_maze_cc(5, 5), 3)
+    seeds = [3, 4, 5]
+    eng.set_state(mt=torch.as_tensor(_mt_rows(seeds).view(np.int32), device=eng.device))
+    start = torch.tensor([[1, 1], [5, 0], [2, 7]], dtype=torch.int32, device=eng.device)
+    maze = eng.generate_maze(start).cpu().numpy()
+    mt = eng.get_state()['mt'].cpu().numpy().view(np.uint32)
+    assert (maze[1] == -1).all() and (maze[2] == -1).all()
+    assert set(np.unique(maze[0])) <= {0, 1} and maze[0, 1, 1] == 0
+    for e in (1, 2):
+        assert np.array_equal(mt[e, :625], _mt_rows([seeds[e]])[0, :625])
