@@ -378,9 +378,15 @@ def main():
         gw_rollout fragments of up to --fragment steps on actions generated
         into HBM before the timed region; HIP events around every launch."""
         F = max(1, min(args.fragment, args.steps))
-        acts = torch.empty((max(F, min(args.fragment, max(untimed, 1))),) + tuple(eng.actions.shape),
-                           dtype=torch.int32, device=eng.device)
-        out = eng.rollout_buffers(acts.shape[0])
+        nfrag = max(F, min(args.fragment, max(untimed, 1)))
+        # ONE action buffer for the pre-roll, the warmup and the timed steps
+        # (a training loop reuses its buffers): the timed fragments read
+        # pages the untimed ones already used, not a fresh allocation whose
+        # first launch pays cold address translation (tools/first_launch_probe2.py)
+        acts_all = torch.empty((max(nfrag, args.steps),) + tuple(eng.actions.shape),
+                               dtype=torch.int32, device=eng.device)
+        acts = acts_all[:nfrag]
+        out = eng.rollout_buffers(nfrag)
         t = 0
         while t < untimed:                  # untimed pre-roll + warmup
             f = min(acts.shape[0], untimed - t)
@@ -391,8 +397,7 @@ def main():
         torch.cuda.synchronize()
         eng.check_errors(allow=allow)
         # the timed steps' actions: inputs resident in HBM before timing
-        all_acts = torch.empty((args.steps,) + tuple(eng.actions.shape), dtype=torch.int32,
-                               device=eng.device)
+        all_acts = acts_all[:args.steps]
         for s in range(args.steps):
             eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
         frags = [(i, min(F, args.steps - i)) for i in range(0, args.steps, F)]
