@@ -387,9 +387,20 @@ def main():
                                dtype=torch.int32, device=eng.device)
         acts = acts_all[:nfrag]
         out = eng.rollout_buffers(nfrag)
+        # untimed pre-roll + warmup as fragments of up to nfrag steps, the
+        # last one exactly F steps: it writes the same output slabs and reads
+        # the same action slabs as the timed fragments, so the timed launch
+        # does not start on cold address translations for them
+        sizes, rest = [], untimed
+        last = min(F, rest)
+        rest -= last
+        while rest > 0:
+            sizes.append(min(nfrag, rest))
+            rest -= sizes[-1]
+        if last:
+            sizes.append(last)
         t = 0
-        while t < untimed:                  # untimed pre-roll + warmup
-            f = min(acts.shape[0], untimed - t)
+        for f in sizes:
             for s in range(f):
                 eng.random_actions(key, t + s, env_offset=first, out=acts[s])
             eng.rollout(acts[:f], horizon=args.horizon, autoreset=mode, skip_done_obs=True, out=out)
