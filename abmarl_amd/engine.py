@@ -351,12 +351,22 @@ class GridWorldEngine:
         assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
         assert autoreset in ('same_step', 'next_step'), autoreset
         out = self.rollout_buffers(K) if out is None else out
+        assert out['obs'].shape[0] >= K, "rollout buffers hold fewer steps than the fragment"
         # self.all_done is in/out: gw_rollout leaves the last step's __all__ in it
         if torch.cuda.current_device() == self.device.index:
-            st = self.L.gw_rollout(
-                self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
-                _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
-                self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream())
+            # the output / engine pointers and the stream are built once per
+            # (out, stream): the host cost of a launch is one ctypes call
+            s = torch.cuda.current_stream().cuda_stream
+            c = getattr(self, '_rollout_args', None)
+            key = (s, out['obs'].data_ptr(), out['reward'].data_ptr(), out['done'].data_ptr(),
+                   out['all_done'].data_ptr())
+            if c is None or c[0] != key:
+                c = self._rollout_args = (
+                    key, None, (_ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                                _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting)),
+                    (_ptr(self.err), C.c_void_p(s)))
+            st = self.L.gw_rollout(self.h, K, C.c_void_p(actions.data_ptr()), *c[2], int(horizon),
+                                   self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), *c[3])
         else:
             with torch.cuda.device(self.device):
                 st = self.L.gw_rollout(
