@@ -2585,6 +2585,15 @@ __global__ void invalidate_cache_kernel(uint32_t* mt, int E)
     if (e < E) mt[(size_t)e * GW_MT_STRIDE + MT_CBASE_SLOT] = 0xFFFFFFFFu;
 }
 
+// F_OBS_M2 is a fact about the engine's own obs buffer, not entity state:
+// a snapshot never carries it and a restore clears it, so the next step
+// rewrites every row (the restored obs buffer need not hold -2 there)
+__global__ void clear_obs_m2_kernel(uint8_t* flags, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] &= (uint8_t)~F_OBS_M2;
+}
+
 __global__ void seed_kernel(uint32_t* mt, const uint32_t* seeds, int E)
 {
     // np.random.seed(int) == init_genrand; one thread per env (once per run)
@@ -2747,6 +2756,7 @@ struct gw_engine {
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
     bool lane_envs;            // lane_step_kernel<S>: MazeNavigation, one lane per env (gw_lane.inc)
+    bool lane_envs_config;     // what gw_create chose (a placement order turns lane_envs off)
     int32_t* d_place_order;    // gw_set_placement_order: [E][A]
     int32_t* d_act_order;      // gw_set_action_order: order [E][A] | rank [E][A]
     size_t smem_lane;          // its dynamic LDS: the per-config tables
@@ -3375,6 +3385,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             return GW_E_UNSUPPORTED;
         }
         g->lane_envs = able && cfg->env_per_lane >= 0;
+        g->lane_envs_config = g->lane_envs;
         if (g->lane_envs) HIPCHK(set_part_attrs(g->S, PK_STEP_LANE, PK_STEP_LANE, g->smem_lane, g->smem_lane));
     }
     *out = g;
@@ -3431,6 +3442,8 @@ gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
         }
     }
     if (!g->d_act_order) HIPCHK(hipMalloc(&g->d_act_order, both.size() * sizeof(int32_t)));
+    // launches already queued on any stream may still read the old order
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(g->d_act_order, both.data(), both.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     g->base.act_order = g->d_act_order;
     g->base.act_rank = g->d_act_order + (size_t)g->E * g->A;
@@ -3440,7 +3453,11 @@ gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
 gw_status gw_set_placement_order(gw_handle g, const int32_t* lane_order, int32_t n)
 {
     if (!g) return GW_E_INVALID;
-    if (n == 0 || !lane_order) { g->base.place_order = nullptr; return GW_OK; }
+    if (n == 0 || !lane_order) {
+        g->base.place_order = nullptr;
+        g->lane_envs = g->lane_envs_config;      // agents-dict order again
+        return GW_OK;
+    }
     if (n != g->E * g->A) { set_err("placement order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
     if (g->wg || g->pacman) {
         set_err("randomize_placement_order runs on the one-wave kernel only");
@@ -3455,6 +3472,8 @@ gw_status gw_set_placement_order(gw_handle g, const int32_t* lane_order, int32_t
         }
     }
     if (!g->d_place_order) HIPCHK(hipMalloc(&g->d_place_order, (size_t)g->E * g->A * sizeof(int32_t)));
+    // launches already queued on any stream may still read the old order
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(g->d_place_order, lane_order, (size_t)g->E * g->A * sizeof(int32_t), hipMemcpyHostToDevice));
     g->base.place_order = g->d_place_order;
     // the one-lane-per-env maze kernel places in lane order: use the one-wave kernel
@@ -3542,7 +3561,11 @@ gw_status gw_get_state(gw_handle g, int32_t* pos, double* health, uint8_t* flags
     const size_t EA = (size_t)g->E * g->A;
     if (pos) HIPCHK(hipMemcpyAsync(pos, g->base.pos, EA * sizeof(int2), hipMemcpyDeviceToDevice, st));
     if (health) HIPCHK(hipMemcpyAsync(health, g->base.health, EA * 8, hipMemcpyDeviceToDevice, st));
-    if (flags) HIPCHK(hipMemcpyAsync(flags, g->base.flags, EA, hipMemcpyDeviceToDevice, st));
+    if (flags) {
+        HIPCHK(hipMemcpyAsync(flags, g->base.flags, EA, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(clear_obs_m2_kernel, dim3((unsigned)((EA + 255) / 256)), dim3(256), 0, st, flags, EA);
+        HIPCHK(hipGetLastError());
+    }
     if (seq) HIPCHK(hipMemcpyAsync(seq, g->base.seq, EA * 4, hipMemcpyDeviceToDevice, st));
     if (mt) HIPCHK(hipMemcpyAsync(mt, g->base.mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));
     if (steps) HIPCHK(hipMemcpyAsync(steps, g->base.steps, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
@@ -3557,7 +3580,12 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     const size_t EA = (size_t)g->E * g->A;
     if (pos) HIPCHK(hipMemcpyAsync(g->base.pos, pos, EA * sizeof(int2), hipMemcpyDeviceToDevice, st));
     if (health) HIPCHK(hipMemcpyAsync(g->base.health, health, EA * 8, hipMemcpyDeviceToDevice, st));
-    if (flags) HIPCHK(hipMemcpyAsync(g->base.flags, flags, EA, hipMemcpyDeviceToDevice, st));
+    if (flags) {
+        HIPCHK(hipMemcpyAsync(g->base.flags, flags, EA, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(clear_obs_m2_kernel, dim3((unsigned)((EA + 255) / 256)), dim3(256), 0, st,
+                           g->base.flags, EA);
+        HIPCHK(hipGetLastError());
+    }
     if (seq) HIPCHK(hipMemcpyAsync(g->base.seq, seq, EA * 4, hipMemcpyDeviceToDevice, st));
     if (mt) {
         HIPCHK(hipMemcpyAsync(g->base.mt, mt, (size_t)g->E * GW_MT_STRIDE * 4, hipMemcpyDeviceToDevice, st));

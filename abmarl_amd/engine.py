@@ -312,6 +312,7 @@ class GridWorldEngine:
         = agents-dict order): PositionState(randomize_placement_order=True)."""
         if lane_order is None:
             _native.check(self.L.gw_set_placement_order(self.h, None, 0), 'gw_set_placement_order')
+            self.kernel = int(self.L.gw_env_kernel(self.h))
             return
         o = np.ascontiguousarray(np.asarray(lane_order, dtype=np.int32).reshape(self.E, self.A))
         _native.check(self.L.gw_set_placement_order(self.h, o.ctypes.data_as(C.c_void_p), o.size),
@@ -338,6 +339,22 @@ class GridWorldEngine:
                     done=torch.empty((n_steps, E, A), dtype=torch.uint8, device=dev),
                     all_done=torch.empty((n_steps, E), dtype=torch.uint8, device=dev))
 
+    def _check_rollout_buffers(self, K, out):
+        """Every slab of `out` holds >= K steps of this engine's shape, on its
+        device (checked when the cached launch arguments change, and for a
+        fragment longer than the slabs last checked)."""
+        E, A = self.E, self.A
+        want = dict(obs=((E, A) + self.obs_shape, torch.int32), reward=((E, A), torch.float64),
+                    done=((E, A), torch.uint8), all_done=((E,), torch.uint8))
+        for k, (shape, dt) in want.items():
+            t = out[k]
+            assert t.dtype == dt and t.is_contiguous() and t.device == self.device, (k, t.dtype, t.device)
+            assert t.dim() == len(shape) + 1 and tuple(t.shape[1:]) == shape, (k, tuple(t.shape), shape)
+            assert t.shape[0] >= K, f"rollout buffer {k!r} holds {t.shape[0]} steps < fragment {K}"
+        self._rollout_cap = min(int(out[k].shape[0]) for k in want)
+
+    _rollout_cap = 0
+
     def rollout(self, actions, horizon=0, autoreset='next_step', skip_done_obs=False, out=None):
         """A fragment of K = actions.shape[0] consecutive steps with auto-reset
         in ONE launch (gw_rollout): the results of K step_autoreset[_next]
@@ -350,8 +367,10 @@ class GridWorldEngine:
         assert actions.dtype == torch.int32 and actions.is_contiguous()
         assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
         assert autoreset in ('same_step', 'next_step'), autoreset
+        assert actions.device == self.device, (actions.device, self.device)
         out = self.rollout_buffers(K) if out is None else out
-        assert out['obs'].shape[0] >= K, "rollout buffers hold fewer steps than the fragment"
+        if K > self._rollout_cap:
+            self._check_rollout_buffers(K, out)
         # self.all_done is in/out: gw_rollout leaves the last step's __all__ in it
         if torch.cuda.current_device() == self.device.index:
             # the output / engine pointers and the stream are built once per
@@ -361,6 +380,7 @@ class GridWorldEngine:
             key = (s, out['obs'].data_ptr(), out['reward'].data_ptr(), out['done'].data_ptr(),
                    out['all_done'].data_ptr())
             if c is None or c[0] != key:
+                self._check_rollout_buffers(K, out)
                 c = self._rollout_args = (
                     key, None, (_ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
                                 _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting)),
@@ -368,6 +388,7 @@ class GridWorldEngine:
             st = self.L.gw_rollout(self.h, K, C.c_void_p(actions.data_ptr()), *c[2], int(horizon),
                                    self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), *c[3])
         else:
+            self._check_rollout_buffers(K, out)
             with torch.cuda.device(self.device):
                 st = self.L.gw_rollout(
                     self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),

@@ -4,12 +4,21 @@ Workload (BASELINE.json configs[2], the metric's config): TeamBattle 32x32,
 64 BattleAgents in 2 teams, 4096 envs per GPU (weak scaling: N GPUs run
 N x 4096 envs, sharded by global env id, no data-path collective;
 --global-envs G: strong scaling, G envs in total), horizon 200 with
-on-device auto-reset.  One timed "step" = random-policy actions (Philox
-kernel) + one fused AllStepManager.step launch for every env.  Before the
-warmup, --preroll steps (default 1000, five horizons) run untimed so that
-the timed window is steady state: episodes at mixed phases, envs resetting
-inside the window.  --workload maze | rtt | pacman times BASELINE configs
-2, 4 and 5 instead (their own lines).
+on-device auto-reset.  Before the warmup, --preroll steps (default 1000,
+five horizons) run untimed so that the timed window is steady state:
+episodes at mixed phases, envs resetting inside the window.
+
+Timed protocol, default --mode rollout (the headline line): the K timed
+steps' random-policy actions (Philox kernel) are generated into HBM BEFORE
+the timed region -- inputs resident in HBM, legitimate for a random policy,
+not for a policy that reads observations -- and the timed region holds only
+gw_rollout launches of --fragment steps each (K = 20 is ONE launch), with
+skip_done_obs: obs rows of entities that get no observation in a step (done
+entities, all_step_manager.py:68-71) are not written.  --mode step (and the
+line's "closed_loop" block) is the RLlib per-step protocol instead: one
+Philox action launch + one fused AllStepManager.step launch per timed step.
+--workload maze | rtt | pacman times BASELINE configs 2, 4 and 5 instead
+(their own lines).
 
 Auto-reset (--autoreset): 'next_step' (default; gymnasium NEXT_STEP, the
 batched form of RLlib calling reset() after __all__: an env whose episode
@@ -98,48 +107,76 @@ def rtt_step_bytes(E, A, S, act_dim):
     return step_bytes(E, A, S) + E * A * (4 * act_dim - 12)
 
 
-def cpu_baseline(cc, seconds=10.0, envs=512, horizon=200, mode='next_step'):
-    """The oracle (C port of the reference step, OpenMP over envs) on this
-    host's cores, bounded to ~`seconds` of work on a sample of the workload,
-    with the same auto-reset flow as the GPU line."""
-    from oracle.oracle import Oracle, lib
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
-    lib().gwo_set_threads(threads)
-    o = Oracle(cc, envs)
-    from abmarl_amd.engine import env_seeds
-    o.seed(env_seeds(envs))
-    E, A, S = envs, cc.n_agents, cc.obs_side
-    obs = o.new_obs()
-    rew = np.zeros((E, A)); done = np.zeros((E, A), np.uint8); ad = np.zeros(E, np.uint8)
-    acting = np.zeros(E, np.uint64)
-    o.reset(obs)
-    rng = np.random.RandomState(7)
-    t0 = time.perf_counter()
-    steps = 0
-    while time.perf_counter() - t0 < seconds:
-        act = np.zeros((E, A, 3), np.int32)
-        act[..., :2] = rng.randint(-1, 2, size=(E, A, 2))
-        act[..., 2] = rng.randint(0, 2, size=(E, A))
-        if mode == 'next_step':
-            rs = (ad != 0) | (o.state()['steps'] >= horizon)
-            if rs.any():
-                o.reset(obs, mask=rs.astype(np.uint8))
-                ad[rs] = 0
-            o.step(act, obs, rew, done, ad, acting, mask=(~rs).astype(np.uint8))
-        else:
-            o.step(act, obs, rew, done, ad, acting)
-            o.reset(obs, all_done=ad, horizon=horizon)
-        steps += 1
-    dt = time.perf_counter() - t0
+def physical_cpus():
+    """One logical CPU per physical core among the CPUs this process may run
+    on (sched_getaffinity; SMT siblings dropped via sysfs topology)."""
+    avail = sorted(os.sched_getaffinity(0))
+    seen, out = set(), []
+    for c in avail:
+        try:
+            sib = open(f'/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list').read().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+    return out, len(avail)
+
+
+def cpu_baseline(cc, seconds=10.0, envs_per_core=64, horizon=200, mode='next_step'):
+    """The C oracle (a port of the reference step) as ONE single-threaded
+    process per physical core, each pinned with sched_setaffinity and running
+    its own envs, for ~`seconds` of wall time, with the same
+    auto-reset flow as the GPU line.  Processes are capped at the job's CPU
+    share (OMP_NUM_THREADS, 16 on the GPU box): the pool gives one GPU job
+    16 cores, so the whole-socket figure is extrapolated from the per-core
+    rate and labelled as such."""
+    import subprocess
+    cores, n_logical = physical_cpus()
+    share = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(cores)
+    use = cores[:max(1, min(share, len(cores)))]
+    procs = []
+    for k, cpu in enumerate(use):
+        cmd = [sys.executable, '-m', 'oracle.cpu_worker', '--cpu', str(cpu), '--seconds', str(seconds),
+               '--envs', str(envs_per_core), '--first-env', str(k * envs_per_core),
+               '--horizon', str(horizon), '--mode', mode]
+        env = dict(os.environ, OMP_NUM_THREADS='1')
+        procs.append(subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, env=env))
+    res = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=seconds * 6 + 120)
+        if pr.returncode != 0:
+            raise RuntimeError(f'cpu_worker failed ({pr.returncode})')
+        res.append(json.loads(out.decode().strip().splitlines()[-1]))
+    per_core = [r['acting'] / r['seconds'] for r in res]
+    total = float(sum(per_core))
     model, ncpu = host_cpu()
-    return dict(value=float(acting.sum()) / dt, unit='agent-steps/s', cores=threads, kind='port',
-                sample=f'{envs} envs x {steps} steps, {mode} auto-reset (incl. action generation '
-                       f'in numpy), {dt:.1f} s, oracle/gw_oracle.c with {threads} OpenMP threads',
-                host_cpu=model, host_logical_cpus=ncpu,
+    # physical cores on the socket(s): distinct (package, core) ids in sysfs
+    phys = set()
+    for c in range(ncpu or 0):
+        try:
+            d = f'/sys/devices/system/cpu/cpu{c}/topology/'
+            phys.add((open(d + 'physical_package_id').read().strip(), open(d + 'core_id').read().strip()))
+        except OSError:
+            pass
+    n_phys = len(phys) or None
+    steps = min(r['steps'] for r in res)
+    return dict(value=total, unit='agent-steps/s', cores=len(use), kind='port',
+                per_core=round(float(np.mean(per_core)), 1),
+                per_core_min=round(float(np.min(per_core)), 1),
+                sample=f'{len(use)} pinned single-threaded processes x {envs_per_core} envs, '
+                       f'>= {steps} steps each, {mode} auto-reset (numpy action generation included), '
+                       f'{seconds:.0f} s each, oracle/gw_oracle.c via oracle/cpu_worker.py',
+                host_cpu=model, host_logical_cpus=ncpu, host_physical_cores=n_phys,
+                affinity_logical_cpus=n_logical,
+                extrapolated_all_physical_cores=(round(float(np.mean(per_core)) * n_phys, 1)
+                                                 if n_phys else None),
                 note=('a C port of the reference step (oracle/), not the reference itself: the '
                       'reference AllStepManager is pure Python and runs about '
                       f'{REFERENCE_RATE_PER_CORE:.0f} agent-steps/s per core (SURVEY §6, measured in '
-                      'the build container); it cannot travel to the GPU box'))
+                      'the build container); it cannot travel to the GPU box.  cores = the job\'s CPU '
+                      'share (one pinned process per physical core in it); '
+                      'extrapolated_all_physical_cores = per_core x every physical core of the host'))
 
 
 def quick_config(name, steps=200, warmup=400):
@@ -420,11 +457,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        host_ms = []
         for (i, f), ev in zip(frags, evs):
+            h0 = time.perf_counter()
             ev[0].record()
             eng.rollout(all_acts[i:i + f], horizon=args.horizon, autoreset=mode, skip_done_obs=True,
                         out=out)
             ev[1].record()
+            host_ms.append((time.perf_counter() - h0) * 1e3)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -443,7 +483,7 @@ def main():
             tot = torch.stack([acts_t[0], tmax[1], acts_t[2]])
         return dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
                     step_ms=launch_ms, step_ms_max=kms[0].item(), steps_per_launch=F,
-                    acting_local=acting)
+                    acting_local=acting, host_launch_ms=float(np.mean(host_ms)))
 
     mode = 'next_step' if turn else args.autoreset
     rollout = args.mode == 'rollout' and not turn
@@ -484,6 +524,7 @@ def main():
         # the committed rocprofv3 evidence of this exact launch shape (a
         # rollout profile is per fragment length: tools/profile.sh ... <F>)
         pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{f"_rollout_f{F}" if rollout else ""}.json')
+        prof = {}
         if args.workload in ('team_battle', 'maze') and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')
@@ -502,6 +543,12 @@ def main():
             # (no event / dispatch time in it)
             roof['rocprof_kernel_ms'] = rocprof_ms
             roof['frac_rocprof'] = round(nbytes / (rocprof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        if traffic and prof.get('algorithmic_bytes_per_launch'):
+            # PMC bytes over the algorithmic bytes of the SAME profiled launch
+            # (its own acting count), not of this run's launch
+            roof['traffic_ratio'] = round(traffic / prof['algorithmic_bytes_per_launch'], 4)
+            roof['traffic_source'] = (f"profiles/{os.path.basename(pmc)} ({prof.get('tag')}: "
+                                      f"{prof.get('workload_args', '')})")
         out = {
             'metric': METRIC,
             'value': round(value, 1),
@@ -523,6 +570,8 @@ def main():
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
             'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
+            'acting_agent_steps': int(acting_all),
+            'host_launch_ms': (round(r['host_launch_ms'], 4) if 'host_launch_ms' in r else None),
             'roofline': roof,
             'episode_stats': stats,
             'autoreset': mode,
@@ -532,7 +581,8 @@ def main():
                 'kernel_ms': round(r2['step_ms_max'], 4)},
             'closed_loop': None if r3 is None else {
                 'protocol': 'one step launch per step (RLlib per-step protocol), Philox action '
-                            'kernel in the timed region, HIP events on every 4th step kernel',
+                            f'kernel in the timed region, HIP events on every {max(1, args.event_every)}'
+                            '-th step kernel',
                 'value': round(r3['acting'] / r3['dt'], 1),
                 'ms_per_step': round(r3['dt'] / args.steps * 1e3, 4),
                 'kernel_ms': round(r3['step_ms_max'], 4)},

@@ -297,7 +297,10 @@ gw_status gw_step_autoreset_next(gw_handle h, const int32_t* actions, int32_t* o
 /* Snapshot / restore of the engine state (device buffers, caller-owned).
      pos     int32[E][A][2]   (row, col)
      health  double[E][A]
-     flags   uint8[E][A]      bit0 in-grid, bit1 live (not in done_agents), bit2 active
+     flags   uint8[E][A]      bit0 in-grid, bit1 live (not in done_agents), bit2 active,
+                              bits3-5 orientation (Pacman program); the engine-internal
+                              bit6 (obs row already -2) is masked out of a snapshot and
+                              cleared by a restore (the next step rewrites every row)
      seq     uint32[E][A]     placement order inside a cell (dict insertion order)
      mt      uint32[E][GW_MT_STRIDE]  key[624], pos at [624], engine-internal after
      steps   int32[E]                                                          */

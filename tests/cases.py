@@ -147,12 +147,3 @@ def team_battle(rows=32, cols=32, n_agents=64, n_teams=2, **kw):
 
 def golden_config(g):
     return build_sim(g['case']).compiled()
-
-
-def replay(runner, g):
-    """Drive any runner with the fixture's actions / reset schedule.
-
-    runner: object with reset(obs, mask) and step(actions) -> (obs, rew, done, all_done, state)
-    Yields per-step (t, outputs) for comparison.
-    """
-    raise NotImplementedError

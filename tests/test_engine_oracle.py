@@ -324,6 +324,15 @@ def test_reach_the_target_config4(oracle_mod):
     assert eng.wg and eng.A == 256
 
 
+def test_reach_the_target_config4_all_8192_envs(oracle_mod):
+    """The bench's 'all 8192 envs on one GPU' launch shape of config 4
+    (bench.py other_configs.reach_the_target_64_all_8192) vs the oracle."""
+    from tests.cases import RTT_CONFIG4
+    kw = {k: v for k, v in RTT_CONFIG4.items() if k != 'kind'}
+    eng = _run_rtt(oracle_mod, kw, E=8192, T=24, horizon=12, run=13)
+    assert eng.wg and eng.A == 256 and eng.E == 8192
+
+
 @pytest.mark.parametrize('kw', [
     # random health, partial accuracy, 2 attacks per cell, crowded: 211 lanes
     dict(rows=24, cols=24, n_barriers=60, n_runners=150,

@@ -231,17 +231,75 @@ def test_maze_placement_state_validation():
     assert registry['state']['MazePlacementState'] is MazePlacementState
 
 
+def _user_multi_maze_classes():
+    """Test-side user code: a simulation written against this repository's
+    component plugin API with the reference MultiMazeNavigation example's
+    rules (abmarl/examples/sim/multi_maze_navigation.py:12-74): a
+    MazePlacementState reset, MoveActor moves (-0.1 on a refused move,
+    -0.01 every step), 1 as the reward of a navigator on the target, done
+    when every navigator is there."""
+    from abmarl_amd.sim.agent_based_simulation import Agent
+    from abmarl_amd.sim.gridworld.base import GridWorldSimulation
+    from abmarl_amd.sim.gridworld.agent import GridObservingAgent, MovingAgent
+    from abmarl_amd.sim.gridworld.components import (
+        MazePlacementState, MoveActor, PositionCenteredEncodingObserver)
+
+    class Runner(GridObservingAgent, MovingAgent):
+        def __init__(self, **kw):
+            super().__init__(move_range=1, **kw)
+
+    class MazeRunners(GridWorldSimulation):
+        def __init__(self, **kw):
+            super().__init__(**kw)
+            self.placement = MazePlacementState(**kw)
+            self.mover = MoveActor(**kw)
+            self.observer = PositionCenteredEncodingObserver(**kw)
+            self.finalize()
+
+        def _arrived(self, aid):
+            return np.array_equal(self.agents[aid].position, self.placement.target_agent.position)
+
+        def reset(self, **kw):
+            self.placement.reset(**kw)
+            self.pending = dict.fromkeys((a.id for a in self.agents.values() if isinstance(a, Agent)), 0)
+
+        def step(self, action_dict, **kw):
+            for aid, act in action_dict.items():
+                # two float64 subtractions in this order (not one of -0.11)
+                if not self.mover.process_action(self.agents[aid], act, **kw):
+                    self.pending[aid] -= 0.1
+                self.pending[aid] -= 0.01
+
+        def get_obs(self, aid, **kw):
+            return dict(self.observer.get_obs(self.agents[aid], **kw))
+
+        def get_reward(self, aid, **kw):
+            r, self.pending[aid] = self.pending[aid], 0
+            return 1 if self._arrived(aid) else r
+
+        def get_done(self, aid, **kw):
+            return self._arrived(aid)
+
+        def get_all_done(self, **kw):
+            return all(self._arrived(a.id) for a in self.agents.values() if isinstance(a, Runner))
+
+        def get_info(self, aid, **kw):
+            return {}
+
+    return MazeRunners, Runner
+
+
 @gpu
 @pytest.mark.parametrize('k', range(len(DATA['trajectories'])))
 def test_multi_maze_navigation_replays_reference(k):
-    """The reference's MultiMazeNavigationSim example, rewritten on this
-    repository's components (abmarl_amd/examples/multi_maze_navigation.py),
+    """The reference's MultiMazeNavigationSim example, rewritten as test-side
+    user code on this repository's components (_user_multi_maze_classes),
     under AllStepManager: every observation, reward bit pattern, done,
     position and the MT19937 state after each step match the reference's
     own trajectory (episodes reset at __all__ or the horizon)."""
     from tests.golden.make_maze import build_multi_maze, multi_maze_actions
-    from abmarl_amd.examples.multi_maze_navigation import MultiMazeNavigationSim, MultiMazeNavigationAgent
     from abmarl_amd.sim.gridworld.agent import GridWorldAgent
+    MultiMazeNavigationSim, MultiMazeNavigationAgent = _user_multi_maze_classes()
     from abmarl_amd.managers import AllStepManager
     t = DATA['trajectories'][k]
     sim = build_multi_maze(t, MultiMazeNavigationSim, MultiMazeNavigationAgent, GridWorldAgent)

@@ -186,6 +186,15 @@ def test_turn_based_config5_vs_oracle(oracle_mod):
     assert resets > 0 and steps > 0
 
 
+def test_turn_based_config5_16384_envs_vs_oracle(oracle_mod):
+    """The bench's config 5 launch shape (16384 envs, TurnBasedManager,
+    next-step auto-reset) for 60 turns, a short horizon so that resets land
+    inside the run."""
+    cc = _sim().compiled()
+    resets, steps = _turn_vs_oracle(oracle_mod, cc, E=16384, T=60, horizon=25, key=37, seed_run=6)
+    assert resets > 0 and steps > 0
+
+
 def test_dict_turn_based_matches_oracle(oracle_mod):
     """TurnBasedManager over the engine-backed PacmanSim (dict API) against the
     oracle's turn protocol from the same np.random seed."""

@@ -92,6 +92,54 @@ def test_rollout_skip_done_obs():
     _compare(a, b, 0, horizon=25, mode='next_step', frags=(20, 20), skip=True)
 
 
+def test_rollout_headline_full_size_bench_shape():
+    """The headline bench's launch shape: 4096 envs, episodes staggered over
+    the 200-step horizon (a reset lands in every step), 20-step fragments,
+    skip_done_obs, next-step auto-reset (bench.py run_rollout)."""
+    a, b = _pair(team_battle(), 4096, run=1, stagger=200)
+    _compare(a, b, 0, horizon=200, mode='next_step', frags=(20, 20), skip=True)
+
+
+def test_rollout_workgroup_kernel_8192_envs():
+    """Config 4's 8192-envs-on-one-GPU launch shape (bench.py
+    other_configs.reach_the_target_64_all_8192) as one 30-step fragment
+    against single steps."""
+    kw = {k: v for k, v in RTT_CONFIG4.items() if k != 'kind'}
+    cc = build_rtt(dict(kind='rtt', **kw)).compiled()
+    a, b = _pair(cc, 8192, run=8, stagger=20)
+    assert a.wg
+    _compare(a, b, 0, horizon=20, mode='next_step', frags=(30,), skip=True, allow_err=True)
+
+
+def test_restored_snapshot_rewrites_done_rows():
+    """A snapshot restored into another engine (gw_get_state -> reset ->
+    gw_set_state): the next step writes every row, so done entities show -2
+    again (the engine-internal obs-row bit does not travel with a snapshot)."""
+    import torch
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    cc = team_battle(rows=8, cols=8, n_agents=40, n_teams=2,
+                     agent=dict(move_range=1, attack_range=1, attack_strength=1,
+                                attack_accuracy=1, view_range=2))
+    E = 256
+    a = GridWorldEngine(cc, E, seeds=env_seeds(E, run=9))
+    b = GridWorldEngine(cc, E, seeds=env_seeds(E, run=10))
+    a.reset()
+    for t in range(12):
+        a.step(a.random_actions(3, t))
+    assert a.done.any().item(), "some entity is done by now"
+    snap = a.get_state()
+    assert not (snap['flags'] & 0x40).any().item(), "snapshot carries the internal bit"
+    b.reset()
+    b.set_state(**snap)
+    act = a.random_actions(3, 12)
+    oa = a.step(act)[0].cpu().numpy()
+    ob = b.step(act)[0].cpu().numpy()
+    assert (oa == ob).all()
+    dead = a.done.cpu().numpy().astype(bool)
+    assert (ob[dead] == -2).all()
+    torch.cuda.synchronize()
+
+
 def test_rollout_dense_small_grid():
     """Crowded 8x8 grid, 40 agents in 3 teams (crowded-cell draws, kills,
     one-team-remaining ends inside fragments)."""
