@@ -33,6 +33,10 @@ GW_OP_MOVE = 3
 GW_OP_ATTACK = 4
 GW_OP_OBSERVE = 5
 GW_OP_MAZE_RESET = 6
+GW_OP_CROSS_MOVE = 7
+GW_OP_DRIFT_MOVE = 8
+GW_OP_ORIENT_RESET = 9
+GW_OP_OBSERVE_ABS = 10
 
 GW_K_OBSERVING = 0x01
 GW_K_ACTING = 0x02

@@ -59,6 +59,37 @@
 #define SEQ_RENORM (1u << 23)
 #define CELL_CROWD 0x80u
 #define CELL_OFF 0xFFu
+// lane_step_kernel (gw_lane.inc): lanes per env for an S x S window (the
+// window's cell count rounded up to 16, 32 or 64; host and device)
+__host__ __device__ constexpr int lane_group(int S) { return S * S <= 16 ? 16 : (S * S <= 32 ? 32 : 64); }
+
+// create_grid_and_mask (utils.py:46-115): does a blocker at offset (rd, cd)
+// from the observer hide the cell at offset (r, c)?  The eight cases differ
+// only in the half-plane scanned and in the +-0.5 offsets of the two rays;
+// the arithmetic is the reference's, in double.  Whether a cell is hidden
+// does not depend on the mask range (the range only bounds the scan), so
+// one function serves every range (host LUTs, device on the fly).
+__host__ __device__ inline bool shadow_hides(int rd, int cd, int r, int c)
+{
+    if ((rd == 0 && cd == 0) || (r == rd && c == cd)) return false;    // not the blocker itself
+    const double r_d = rd, c_d = cd;
+    if (cd == 0) {                                          // below / above: rays in c
+        if (rd > 0 ? r < rd : r > rd) return false;
+        const double dd = rd > 0 ? -0.5 : 0.5;
+        const double left = (c_d - 0.5) / (r_d + dd) * r, right = (c_d + 0.5) / (r_d + dd) * r;
+        return left < c && c < right;
+    }
+    if (cd > 0 ? c < cd : c > cd) return false;             // rays in r
+    if (rd > 0 && r < rd) return false;
+    if (rd < 0 && r > rd) return false;
+    // offsets of (rd -+ 0.5) / (cd + lo_d | up_d) per case
+    double lo_d, up_d;
+    if (rd == 0) { lo_d = up_d = cd > 0 ? -0.5 : 0.5; }             // right / left
+    else if ((rd > 0) == (cd > 0)) { lo_d = 0.5; up_d = -0.5; }     // below-right / above-left
+    else { lo_d = -0.5; up_d = 0.5; }                               // below-left / above-right
+    const double lo = (r_d - 0.5) / (c_d + lo_d) * c, up = (r_d + 0.5) / (c_d + up_d) * c;
+    return lo < r && r < up;
+}
 
 namespace {
 
@@ -2465,6 +2496,88 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     STAMP_WAVE(61, false);
 }
 
+// CrossMoveActor.grid_action (actor.py:142-159): 0 stay, 1 left, 2 down, 3 right, 4 up
+__device__ __forceinline__ int cross_row(int d) { return d == 2 ? 1 : (d == 4 ? -1 : 0); }
+__device__ __forceinline__ int cross_col(int d) { return d == 1 ? -1 : (d == 3 ? 1 : 0); }
+
+// AbsoluteEncodingObserver.get_obs (observer.py:95-150) for lane a (uniform)
+// into out[H][W]: -2 outside the view range and behind blockers (every
+// active blocking entity, create_grid_and_mask evaluated per cell with
+// shadow_hides, so any view range), -1 the observer's own cell (no draw), 0
+// empty, a lone occupant's encoding, and for a crowded cell
+// np.random.choice over its occupants' encodings in insertion (seq) order,
+// the draws in the window's row-major order (the reference's loop).
+__device__ __forceinline__ void observe_absolute(const Params& p, const Smem& sm, Rng& rng, const Lane& L,
+                                                 int a, int v, int32_t* out)
+{
+    const int l = lane_id(), A = p.A;
+    const int ra = rl(L.r, a), ca = rl(L.c, a);
+    const bool a_in = rlb(L.in_grid, a);
+    const int self = a_in ? ra * p.W + ca : -1;
+    const int r0 = ra - v > 0 ? ra - v : 0, r1 = ra + v < p.H - 1 ? ra + v : p.H - 1;
+    const int c0 = ca - v > 0 ? ca - v : 0, c1 = ca + v < p.W - 1 ? ca + v : p.W - 1;
+    const uint64_t blk = __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING));
+    auto hidden = [&](int gr, int gc) -> bool {
+        bool h = false;
+        for (uint64_t it = blk; it; it &= it - 1) {
+            const int b = first_lane(it);
+            const int dr = rl(L.r, b) - ra, dc = rl(L.c, b) - ca;
+            if (dr >= -v && dr <= v && dc >= -v && dc <= v && shadow_hides(dr, dc, gr - ra, gc - ca))
+                h = true;
+        }
+        return h;
+    };
+    // crowded cells (>= 2 occupants, so a lane is there) ranked by cell index
+    const int my = L.r * p.W + L.c;
+    const bool crowded = l < A && L.in_grid && cnt_get(sm.cnt, my) >= 2;
+    bool rep = crowded;
+    for (uint64_t it = __ballot(crowded); it; it &= it - 1) {
+        const int i = first_lane(it);
+        if (crowded && i < l && rl(my, i) == my) rep = false;
+    }
+    const uint64_t reps = __ballot(rep);
+    int rank = 0;
+    for (uint64_t it = reps; it; it &= it - 1) {
+        const int i = first_lane(it);
+        if (rep && rl(my, i) < my) rank++;
+    }
+    const int ncl = __popcll(reps);
+    int ccell = -1, cval = 0;                 // lane j: the j-th crowded cell and its value
+    for (int j = 0; j < ncl; j++) {
+        const int cell = rl(my, first_lane(__ballot(rep && rank == j)));
+        const int gr = cell / p.W, gc = cell - gr * p.W;
+        int val = -2;
+        if (gr >= r0 && gr <= r1 && gc >= c0 && gc <= c1 && cell != self && !hidden(gr, gc)) {
+            const uint32_t kk = rng.interval(cnt_get(sm.cnt, cell) - 1u);
+            const bool in = l < A && L.in_grid && my == cell;
+            uint32_t below = 0;
+            for (uint64_t it = __ballot(in); it; it &= it - 1) {
+                const int i = first_lane(it);
+                if (in && rl(L.seq, i) < L.seq) below++;
+            }
+            val = rl(L.enc, first_lane(__ballot(in && below == kk)));
+        }
+        if (l == j) { ccell = cell; cval = val; }
+    }
+    const int HW = p.H * p.W;
+    for (int i = l; i < HW; i += WAVE) {
+        const int gr = i / p.W, gc = i - gr * p.W;
+        int val;
+        if (gr < r0 || gr > r1 || gc < c0 || gc > c1 || hidden(gr, gc)) {
+            val = -2;
+        } else if (i == self) {
+            val = -1;
+        } else {
+            const uint32_t b = sm.tbl[tbl_idx(p, gr, gc)];
+            val = (int)b;
+            if (b == CELL_CROWD)
+                for (int j = 0; j < ncl; j++)
+                    if (rl(ccell, j) == i) val = rl(cval, j);
+        }
+        out[i] = val;
+    }
+}
+
 // The component plugin API (state.py / actor.py / observer.py), one
 // component call for ONE entity (lane p.obs_only) in every env: the wave
 // loads the env, runs the component's body as the fused programs do, and
@@ -2487,6 +2600,7 @@ __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
     const int op = p.mode, a = p.obs_lane;
     int32_t* res = p.comp_out ? p.comp_out + (size_t)e * (2 + A) : nullptr;
     int status = 0, nlist = 0, list = -1;
+    int res2 = -1;                            // DRIFT_MOVE: result[2], the orientation
     uint32_t err = 0;
     // the component's own parameters come with the call (gw_engine.h)
     const int32_t* arg = p.actions ? p.actions + (size_t)e * p.act_dim : nullptr;
@@ -2532,6 +2646,62 @@ __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
                 if (l == a) L.amap = keep;
                 status = st ? 1 : 0;
             }
+        } else if (op == GW_OP_CROSS_MOVE || op == GW_OP_DRIFT_MOVE) {
+            // CrossMoveActor / DriftMoveActor.process_action (actor.py:161-234):
+            // arg[0] the cross action, arg[1] (drift) the agent's orientation
+            // (0 = None); status -1 None for an agent of another type, -2 a
+            // drift with no orientation (the reference's AssertionError);
+            // result[1] = 1 when the drift ran (action_dict['move'] was
+            // replaced by the orientation), result[2] = the new orientation
+            const uint32_t ak = (uint32_t)rl((int32_t)L.kind, a);
+            const int cross = uni(arg[0]);
+            const bool drift = op == GW_OP_DRIFT_MOVE;
+            int orient = drift ? uni(arg[1]) : 0;
+            const bool in = rlb(L.in_grid, a);
+            const int ar = rl(L.r, a), ac = rl(L.c, a);
+            auto cross_move = [&](int d) -> bool {
+                const bool ok = move_one(p, L, a, cross_row(d), cross_col(d), ctr + (uint32_t)a);
+                // a move off a cell the agent is not in: Grid.remove raises KeyError
+                if (ok && !in && (rl(L.r, a) != ar || rl(L.c, a) != ac)) {
+                    err |= GW_ERR_NOT_IN_GRID;
+                    if (l == a) { L.r = ar; L.c = ac; }
+                }
+                if (ok && l == a && (L.r != ar || L.c != ac)) L.in_grid = true;
+                return ok;
+            };
+            if (!(ak & GW_K_MOVING) || (drift && !(ak & GW_K_ORIENTATION))) {
+                status = -1;
+            } else if (!drift) {
+                status = cross_move(cross) ? 1 : 0;
+            } else if (cross != 0 && cross_move(cross)) {
+                orient = cross;
+                status = 1;
+            } else if (orient < 1 || orient > 4) {
+                status = -2;
+            } else {
+                nlist = 1;
+                status = cross_move(orient) ? 1 : 0;
+            }
+            if (drift) res2 = orient;
+            ctr += (uint32_t)WAVE;
+        } else if (op == GW_OP_ORIENT_RESET) {
+            // OrientationState.reset (state.py:666-675): initial_orientation or
+            // np.random.randint(1, 5), OrientationAgents in agent order;
+            // result[2 + lane] = the lane's orientation (0 for other lanes)
+            int o = 0;
+            for (uint64_t it = __ballot(valid && (L.kind & GW_K_ORIENTATION)); it; it &= it - 1) {
+                const int b = first_lane(it);
+                int ob = p.spec[b].init_orient;
+                if (ob == 0) ob = 1 + (int)rng.interval(3u);
+                if (l == b) o = ob;
+            }
+            status = 1;
+            nlist = A;
+            list = o;
+        } else if (op == GW_OP_OBSERVE_ABS) {
+            // arg[0]: the observer's view range (any range; the spec's is capped)
+            observe_absolute(p, sm, rng, L, a, arg ? uni(arg[0]) : rl(L.view, a),
+                             p.obs + ((size_t)e * A + a) * p.H * p.W);
         } else if (op == GW_OP_OBSERVE) {
             if (arg) q.observe_self = uni(arg[0]);
             q.obs_only = a;
@@ -2543,6 +2713,7 @@ __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
     if (res) {
         if (l == 0) { res[0] = status; res[1] = nlist; }
         if (l < nlist && l < A) res[2 + l] = list;
+        if (res2 >= 0 && l == 0) res[2] = res2;
     }
     if (l == 0 && p.err && err) p.err[e] |= err;
     store_lane(p, e, L, valid);
@@ -2770,37 +2941,15 @@ struct gw_engine {
 };
 
 // create_grid_and_mask (utils.py:46-115): the window cells of range R that a
-// blocker at offset (rd, cd) hides, as bits k = (r+R)(2R+1) + (c+R).  The
-// eight cases differ only in the half-plane scanned and in the +-0.5
-// offsets of the two rays; the arithmetic is the reference's, in double.
+// blocker at offset (rd, cd) hides, as bits k = (r+R)(2R+1) + (c+R)
+// (shadow_hides, the reference's arithmetic in double).
 static void host_shadow(int R, int rd, int cd, uint32_t* bits)
 {
     const int D = 2 * R + 1;
     for (int w = 0; w < mask_words(R); w++) bits[w] = 0u;
-    if (rd == 0 && cd == 0) return;
-    const double r_d = rd, c_d = cd;
     for (int r = -R; r <= R; r++) {
         for (int c = -R; c <= R; c++) {
-            if (r == rd && c == cd) continue;                      // not the blocker itself
-            bool hide = false;
-            if (cd == 0) {                                          // below / above: rays in c
-                if (rd > 0 ? r < rd : r > rd) continue;
-                const double dd = rd > 0 ? -0.5 : 0.5;
-                const double left = (c_d - 0.5) / (r_d + dd) * r, right = (c_d + 0.5) / (r_d + dd) * r;
-                hide = left < c && c < right;
-            } else {                                                // rays in r
-                if (cd > 0 ? c < cd : c > cd) continue;
-                if (rd > 0 && r < rd) continue;
-                if (rd < 0 && r > rd) continue;
-                // offsets of (rd -+ 0.5) / (cd + lo_d | up_d) per case
-                double lo_d, up_d;
-                if (rd == 0) { lo_d = up_d = cd > 0 ? -0.5 : 0.5; }             // right / left
-                else if ((rd > 0) == (cd > 0)) { lo_d = 0.5; up_d = -0.5; }     // below-right / above-left
-                else { lo_d = -0.5; up_d = 0.5; }                               // below-left / above-right
-                const double lo = (r_d - 0.5) / (c_d + lo_d) * c, up = (r_d + 0.5) / (c_d + up_d) * c;
-                hide = lo < r && r < up;
-            }
-            if (hide) {
+            if (shadow_hides(rd, cd, r, c)) {
                 const int k = (r + R) * D + (c + R);
                 bits[k >> 5] |= 1u << (k & 31);
             }
@@ -2839,7 +2988,8 @@ static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const P
 {
     if (g->S < 1 || g->S > 15 || !(g->S & 1)) return hipErrorInvalidValue;
     const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET) ? WAVE * p.nwv : WAVE;
-    const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + WAVE - 1) / WAVE) : (unsigned)g->E;
+    const int epw = WAVE / lane_group(g->S);        // lane_step_kernel: envs per wave
+    const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + epw - 1) / epw) : (unsigned)g->E;
     return k_part_launch[g->S >> 1](kind, grid, block, smem, st, &p);
 }
 
@@ -3377,7 +3527,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         const size_t nsm = (p.blockers && p.smask_off[R] >= 0) ? (size_t)HW * MWS : 0;
         g->smem_lane = 16 * (size_t)((p.tbl_rows * p.pitch + 15) / 16) + 4 * ((nsm + 3) & ~(size_t)3) +
                        (p.static_bits ? 4 * (size_t)((HW + 31) / 32) : 0);
-        const size_t static_lds = (size_t)WAVE * 2 * S * S + 4 * GW_MT_N;
+        const size_t static_lds = 4 * GW_MT_N;
         if (g->smem_lane + static_lds > 64 * 1024) able = false;
         if (cfg->env_per_lane > 0 && !able) {
             set_err("env_per_lane: the one-lane-per-env kernel runs MazeNavigation with the navigator and "
@@ -3768,7 +3918,7 @@ gw_status gw_generate_maze(gw_handle g, const int32_t* start, int8_t* maze, void
 gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
                        int32_t* obs, uint32_t* err_flags, void* stream)
 {
-    if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_MAZE_RESET) return GW_E_INVALID;
+    if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_OBSERVE_ABS) return GW_E_INVALID;
     if (g->wg || g->pacman) {
         set_err("component operations run on the one-wave engine (not the workgroup / Pacman kernels)");
         return GW_E_UNSUPPORTED;
@@ -3781,11 +3931,13 @@ gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* arg
         }
         return maze_launch(g, 1, args, nullptr, nullptr, result, err_flags, (hipStream_t)stream);
     }
-    const bool needs_lane = op == GW_OP_MOVE || op == GW_OP_ATTACK || op == GW_OP_OBSERVE;
+    const bool moves = op == GW_OP_MOVE || op == GW_OP_CROSS_MOVE || op == GW_OP_DRIFT_MOVE;
+    const bool needs_lane = moves || op == GW_OP_ATTACK || op == GW_OP_OBSERVE || op == GW_OP_OBSERVE_ABS;
     if (needs_lane && (lane < 0 || lane >= g->A)) { set_err("lane %d outside 0..%d", lane, g->A - 1); return GW_E_INVALID; }
-    if ((op == GW_OP_MOVE || op == GW_OP_ATTACK) && !args) return GW_E_INVALID;
-    if (op == GW_OP_ATTACK && g->base.act_dim < 3) return GW_E_INVALID;
-    if (op == GW_OP_OBSERVE && !obs) return GW_E_INVALID;
+    if ((moves || op == GW_OP_ATTACK) && !args) return GW_E_INVALID;
+    if ((op == GW_OP_ATTACK || op == GW_OP_DRIFT_MOVE) && g->base.act_dim < 3) return GW_E_INVALID;
+    if ((op == GW_OP_OBSERVE || op == GW_OP_OBSERVE_ABS) && !obs) return GW_E_INVALID;
+    if (op == GW_OP_ORIENT_RESET && !result) return GW_E_INVALID;
     Params p = g->base;
     p.mode = op; p.obs_lane = lane; p.actions = args; p.comp_out = result; p.obs = obs; p.err = err_flags;
     p.nsteps = 1;

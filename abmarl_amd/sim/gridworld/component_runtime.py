@@ -64,7 +64,7 @@ class ComponentRuntime:
         sig.append(tuple((a.encoding, getattr(a, 'view_range', None), getattr(a, 'move_range', None),
                           getattr(a, 'attack_range', None), getattr(a, 'attack_strength', None),
                           getattr(a, 'attack_accuracy', None), getattr(a, 'simultaneous_attacks', None),
-                          getattr(a, 'initial_health', None),
+                          getattr(a, 'initial_health', None), getattr(a, 'initial_orientation', None),
                           None if a.initial_position is None else tuple(a.initial_position), a.blocking)
                          for a in agents.values()))
         return tuple(sig)
@@ -79,9 +79,15 @@ class ComponentRuntime:
             raise ComponentError("the component runtime holds at most 64 entities per grid")
         # selective actions need the (2r+1)^2 action row; binary uses args[2] only
         kind = _abi.GW_ATTACK_SELECTIVE if sig[2] else _abi.GW_ATTACK_BINARY
-        views = [a.view_range for a in agents.values() if isinstance(a, GridObservingAgent)]
+        # the position-centred window is capped at GW_MAX_RANGE; the absolute
+        # observer takes its view range with each call (any range)
+        views = [min(a.view_range, _abi.GW_MAX_RANGE) for a in agents.values()
+                 if isinstance(a, GridObservingAgent)]
+        specs = [agent_spec(a) for a in agents.values()]
+        for s_ in specs:
+            s_.view_range = min(s_.view_range, _abi.GW_MAX_RANGE)
         cc = _abi.CompiledConfig(
-            grid.rows, grid.cols, [agent_spec(a) for a in agents.values()], _abi.GW_SIM_TEAM_BATTLE,
+            grid.rows, grid.cols, specs, _abi.GW_SIM_TEAM_BATTLE,
             grid.overlap_bits(), {}, done_kind=_abi.GW_DONE_ACTIVE,
             obs_range=max(views) if views else 0, attack_kind=kind)
         cc.cfg.all_lanes = 1
@@ -159,7 +165,8 @@ class ComponentRuntime:
 
     # ----------------------------------------------------------- operations
     def op(self, op, agent=None, args=None):
-        """Run one component operation; returns (status, attacked agents, err)."""
+        """Run one component operation; returns (status, attacked agents, err)
+        (the raw result row stays in self.last_result)."""
         lane = -1 if agent is None else self.index[agent.id]
         self._upload()
         if args is not None:
@@ -168,15 +175,29 @@ class ComponentRuntime:
             a[0, :flat.size] = flat
             self.args.copy_(torch.as_tensor(a, device=self.dev))
         self.eng.err.zero_()
-        self.eng.component(op, lane, self.args if args is not None else None, self.result,
-                           self.obs if op == _abi.GW_OP_OBSERVE else None)
-        res = self.result[0].cpu().numpy()
+        obs = self.obs if op == _abi.GW_OP_OBSERVE else (self._abs_obs() if op == _abi.GW_OP_OBSERVE_ABS else None)
+        self.eng.component(op, lane, self.args if args is not None else None, self.result, obs)
+        res = self.last_result = self.result[0].cpu().numpy()
         err = int(self.eng.err[0].item())
         self._download(op)
         attacked = [self.agents[self.ids[int(x)]] for x in res[2:2 + int(res[1])]]
         return int(res[0]), attacked, err
 
+    def _abs_obs(self):
+        if getattr(self, 'abs_obs', None) is None:
+            self.abs_obs = torch.full((1, len(self.ids), self.grid.rows, self.grid.cols), -2,
+                                      dtype=torch.int32, device=self.dev)
+        return self.abs_obs
+
+    def observe_absolute(self, agent):
+        """AbsoluteEncodingObserver.get_obs(agent): the (rows, cols) grid."""
+        self.op(_abi.GW_OP_OBSERVE_ABS, agent, [int(agent.view_range)])
+        return self.abs_obs[0, self.index[agent.id]].cpu().numpy().astype(int)
+
     def observe(self, agent, observe_self=True):
+        if agent.view_range > _abi.GW_MAX_RANGE:
+            raise ComponentError(f"PositionCenteredEncodingObserver: view_range {agent.view_range} > "
+                                 f"{_abi.GW_MAX_RANGE} has no device window")
         self.op(_abi.GW_OP_OBSERVE, agent, [int(observe_self)])
         d = 2 * agent.view_range + 1
         return self.obs[0, self.index[agent.id], :d, :d].cpu().numpy().astype(int)

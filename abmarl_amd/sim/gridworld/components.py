@@ -11,8 +11,8 @@ space assignment.  They run on the engine two ways:
     the agents and the Grid they were built with; the done components read
     that state.
 
-Reference: abmarl/sim/gridworld/state.py:13-166,622-641; actor.py:13-114,
-237-501; observer.py:13-52,153-250; done.py:10-153.
+Reference: abmarl/sim/gridworld/state.py:13-166,622-641,659-675;
+actor.py:13-234,237-501; observer.py:13-250; done.py:10-153.
 """
 import random
 from abc import ABC, abstractmethod
@@ -200,6 +200,19 @@ class HealthState(StateBaseComponent):
 class OrientationState(StateBaseComponent):
     """state.py:659-675: initial_orientation or np.random.randint(1, 5)."""
 
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        register_component(self)
+
+    def reset(self, **kwargs):
+        """gw_component ORIENT_RESET: the draws on the device, in agent order."""
+        rt = ComponentRuntime.of(self)
+        rt.op(_abi.GW_OP_ORIENT_RESET)
+        res = rt.last_result
+        for aid, agent in self.agents.items():
+            if isinstance(agent, OrientationAgent):
+                agent.orientation = int(res[2 + rt.index[aid]])
+
 
 # ----------------------------------------------------------------- actors
 class ActorBaseComponent(GridWorldBaseComponent, _EngineExecuted, ABC):
@@ -259,6 +272,24 @@ class CrossMoveActor(ActorBaseComponent):
             if isinstance(agent, self.supported_agent_type):
                 agent.action_space[self.key] = Discrete(5)
                 agent.null_action[self.key] = 0
+        register_component(self)
+
+    @staticmethod
+    def _check_cross(cross_action):
+        # CrossMoveActor.grid_action (actor.py:152)
+        assert cross_action in [0, 1, 2, 3, 4], "Cross action must be 0, 1, 2, 3, or 4."
+
+    def process_action(self, agent, action_dict, **kwargs):
+        """True if the move succeeded (gw_component CROSS_MOVE); None for
+        agents that are not MovingAgents (actor.py:161-192)."""
+        if not isinstance(agent, self.supported_agent_type):
+            return None
+        cross = action_dict[self.key]
+        self._check_cross(cross)
+        status, _, err = ComponentRuntime.of(self).op(_abi.GW_OP_CROSS_MOVE, agent, [int(cross)])
+        if err & _abi.GW_ERR_NOT_IN_GRID:
+            raise KeyError(agent.id)                  # Grid.remove of an agent not in its cell
+        return bool(status)
 
     @property
     def key(self):
@@ -272,6 +303,29 @@ class CrossMoveActor(ActorBaseComponent):
 class DriftMoveActor(CrossMoveActor):
     """actor.py:195-234: a failed or absent change of direction drifts the
     agent one cell along its orientation (OrientationAgent + MovingAgent)."""
+
+    def process_action(self, agent, action_dict, **kwargs):
+        """gw_component DRIFT_MOVE: the change of direction, else the drift
+        along the orientation (which, as in the reference, replaces
+        action_dict['move']); None for agents that are not Orientation +
+        Moving."""
+        if not (isinstance(agent, OrientationAgent) and isinstance(agent, MovingAgent)):
+            return None
+        cross = action_dict[self.key]
+        if cross != 0:
+            self._check_cross(cross)
+        rt = ComponentRuntime.of(self)
+        status, _, err = rt.op(_abi.GW_OP_DRIFT_MOVE, agent, [int(cross), int(agent.orientation or 0)])
+        res = rt.last_result
+        if res[1] or status == -2:
+            action_dict[self.key] = agent.orientation     # actor.py:233
+        if status == -2:
+            self._check_cross(agent.orientation)          # no orientation: the reference's assert
+        if err & _abi.GW_ERR_NOT_IN_GRID:
+            raise KeyError(agent.id)
+        if int(res[2]) != (agent.orientation or 0):
+            agent.orientation = int(res[2])               # actor.py:229-230
+        return bool(status)
 
 
 class AttackActorBaseComponent(ActorBaseComponent, ABC):
@@ -404,6 +458,15 @@ class AbsoluteEncodingObserver(ObserverBaseComponent):
                 agent.observation_space[self.key] = Box(
                     -2, max_encoding, (self.rows, self.cols), int)
                 agent.null_observation[self.key] = -2 * np.ones((self.rows, self.cols), dtype=int)
+        register_component(self)
+
+    def get_obs(self, agent, **kwargs):
+        """The (rows, cols) grid (gw_component OBSERVE_ABS: blocking masks and
+        crowded-cell draws on the device, in the reference's order); {} for
+        agents that are not GridObservingAgents."""
+        if not isinstance(agent, self.supported_agent_type):
+            return {}
+        return {self.key: ComponentRuntime.of(self).observe_absolute(agent)}
 
     @property
     def key(self):

@@ -366,6 +366,32 @@ gw_status gw_random_actions(gw_handle h, uint64_t key, uint32_t step, uint32_t e
  *                         result[e][0] = 1 placed, 0 raised (err_flags:
  *                         GW_ERR_NO_CELL / GW_ERR_INIT_POSITION).               */
 #define GW_OP_MAZE_RESET     6
+/*   GW_OP_CROSS_MOVE      CrossMoveActor.process_action(lane, {'move': args[e][0]})
+ *                         (actor.py:161-192): 0 stay, 1 left, 2 down, 3 right, 4 up
+ *                         (the host asserts the range, actor.py:152); result[e][0]
+ *                         as GW_OP_MOVE
+ *   GW_OP_DRIFT_MOVE      DriftMoveActor.process_action (actor.py:208-234):
+ *                         args[e][0] the cross action, args[e][1] the agent's
+ *                         orientation (1..4, 0 = None); result[e][0] 1 / 0 / -1
+ *                         None (not Orientation + Moving) / -2 a drift without an
+ *                         orientation (the reference's AssertionError),
+ *                         result[e][1] = 1 when the drift ran (the reference then
+ *                         replaced action_dict['move'] by the orientation),
+ *                         result[e][2] = the orientation afterwards
+ *   GW_OP_ORIENT_RESET    OrientationState.reset (state.py:666-675): initial or
+ *                         np.random.randint(1, 5) per OrientationAgent in agent
+ *                         order; result[e][2 + lane] = the lane's orientation (0:
+ *                         not an OrientationAgent); result required
+ *   GW_OP_OBSERVE_ABS     AbsoluteEncodingObserver.get_obs(lane) (observer.py:95-150),
+ *                         blocking entities included, any view range (args[e][0];
+ *                         NULL args: the spec's): writes obs[e][lane][rows][cols]
+ *                         (obs device int32[E][A][rows][cols])
+ *   The orientation lives with the caller (the component runtime uploads it
+ *   per call); the engine's flags keep no orientation for these handles.   */
+#define GW_OP_CROSS_MOVE     7
+#define GW_OP_DRIFT_MOVE     8
+#define GW_OP_ORIENT_RESET   9
+#define GW_OP_OBSERVE_ABS   10
 gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
                        int32_t* obs, uint32_t* err_flags, void* stream);
 

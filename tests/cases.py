@@ -147,3 +147,42 @@ def team_battle(rows=32, cols=32, n_agents=64, n_teams=2, **kw):
 
 def golden_config(g):
     return build_sim(g['case']).compiled()
+
+
+def shadow_mask(agent, agents, v):
+    """create_grid_and_mask's mask (utils.py:46-115) for `agent` at range v,
+    restated on the host as a test reference: visible(dr, dc).  Each active
+    blocking agent at offset (rd, cd) hides the cells strictly between its
+    two rays (the reference's double arithmetic, eight cases)."""
+    import numpy as np
+    hidden = np.zeros((2 * v + 1, 2 * v + 1), dtype=bool)
+    for other in agents.values():
+        if not (other.active and other.blocking):
+            continue
+        rd, cd = (int(x) for x in np.asarray(other.position) - np.asarray(agent.position))
+        if not (-v <= rd <= v and -v <= cd <= v) or (rd == 0 and cd == 0):
+            continue
+        for r in range(-v, v + 1):
+            for c in range(-v, v + 1):
+                if (r, c) == (rd, cd):
+                    continue
+                if cd == 0:
+                    if (rd > 0 and r < rd) or (rd < 0 and r > rd):
+                        continue
+                    dd = -0.5 if rd > 0 else 0.5
+                    hide = (cd - 0.5) / (rd + dd) * r < c < (cd + 0.5) / (rd + dd) * r
+                else:
+                    if (cd > 0 and c < cd) or (cd < 0 and c > cd):
+                        continue
+                    if (rd > 0 and r < rd) or (rd < 0 and r > rd):
+                        continue
+                    if rd == 0:
+                        lo_d = up_d = -0.5 if cd > 0 else 0.5
+                    elif (rd > 0) == (cd > 0):
+                        lo_d, up_d = 0.5, -0.5
+                    else:
+                        lo_d, up_d = -0.5, 0.5
+                    hide = (rd - 0.5) / (cd + lo_d) * c < r < (rd + 0.5) / (cd + up_d) * c
+                if hide:
+                    hidden[r + v, c + v] = True
+    return lambda dr, dc: not hidden[dr + v, dc + v]
