@@ -187,6 +187,7 @@ struct Params {
     // of OBSERVE (-1 otherwise: every live observer)
     int32_t* comp_out;
     int32_t obs_only;
+    int32_t comp_amap;                     // wg_comp_kernel ATTACK: the attacker's attack_mapping bits (-1: the table's)
     int32_t hetero_view;
     const uint32_t* hshadow;
     const uint32_t* hsmask;
@@ -2864,7 +2865,8 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 // in their own translation unit (-DGW_PART_S=<S>; _native.build compiles the
 // parts in parallel and links them with the host part).  Each part exports a
 // launcher and an attribute setter; the host part dispatches on S to them.
-enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5, PK_STEP_LANE = 6 };
+enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5, PK_STEP_LANE = 6,
+                  PK_WG_COMP = 7 };
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
@@ -2891,6 +2893,7 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_COMP: hipLaunchKernelGGL(comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_STEP_LANE: hipLaunchKernelGGL(lane_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_WG_COMP: hipLaunchKernelGGL(wg_comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2905,6 +2908,7 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
                   : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
                   : kind == PK_COMP ? (const void*)comp_kernel<S>
                   : kind == PK_STEP_LANE ? (const void*)lane_step_kernel<S>
+                  : kind == PK_WG_COMP ? (const void*)wg_comp_kernel<S>
                                        : (const void*)wg_reset_kernel<S>;
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
@@ -2987,7 +2991,7 @@ static const part_attr_fn k_part_attr[8] = {
 static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const Params& p, hipStream_t st)
 {
     if (g->S < 1 || g->S > 15 || !(g->S & 1)) return hipErrorInvalidValue;
-    const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET) ? WAVE * p.nwv : WAVE;
+    const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET || kind == PK_WG_COMP) ? WAVE * p.nwv : WAVE;
     const int epw = WAVE / lane_group(g->S);        // lane_step_kernel: envs per wave
     const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + epw - 1) / epw) : (unsigned)g->E;
     return k_part_launch[g->S >> 1](kind, grid, block, smem, st, &p);
@@ -3136,8 +3140,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // when the config forces it: the parity tests run small reference
     // fixtures through it)
     const bool tb = cfg->sim_kind == GW_SIM_TEAM_BATTLE;
+    // (a component-API handle, every entity a lane, runs only gw_component
+    // operations: either attack kind)
     const bool wg_able = (rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE) ||
-                         (tb && cfg->attack_kind == GW_ATTACK_BINARY);
+                         (tb && cfg->attack_kind == GW_ATTACK_BINARY) ||
+                         (cfg->all_lanes && (rtt || tb));
     if (cfg->force_workgroup && !wg_able) {
         set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor "
                 "and TeamBattle with BinaryAttackActor");
@@ -3267,6 +3274,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.attack_kind = cfg->attack_kind;
     p.persistent_obs = cfg->persistent_obs != 0;
     p.obs_only = -1;
+    p.comp_amap = -1;
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
@@ -3501,7 +3509,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
     HIPCHK(hipMemset(p.racc, 0, EA * sizeof(double)));
-    if (wg) HIPCHK(set_part_attrs(g->S, PK_WG_STEP, PK_WG_RESET, g->smem_step, g->smem_step));
+    if (wg) {
+        HIPCHK(set_part_attrs(g->S, PK_WG_STEP, PK_WG_RESET, g->smem_step, g->smem_step));
+        HIPCHK(set_part_attrs(g->S, PK_WG_COMP, PK_WG_COMP, g->smem_step, g->smem_step));
+    }
     else if (!pac) HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
     g->step_tb = GW_STEP_SPEC && !wg && !pac && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
@@ -3919,11 +3930,12 @@ gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* arg
                        int32_t* obs, uint32_t* err_flags, void* stream)
 {
     if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_OBSERVE_ABS) return GW_E_INVALID;
-    if (g->wg || g->pacman) {
-        set_err("component operations run on the one-wave engine (not the workgroup / Pacman kernels)");
+    if (g->pacman) {
+        set_err("component operations run on the one-wave and workgroup engines (not the Pacman kernel)");
         return GW_E_UNSUPPORTED;
     }
     if (op == GW_OP_MAZE_RESET) {
+        if (g->wg) { set_err("MazePlacementState runs on the one-wave engine (at most 64 entities)"); return GW_E_UNSUPPORTED; }
         if (!args || g->base.act_dim < 3) return GW_E_INVALID;
         if (g->n_ent != g->A) {
             set_err("MazePlacementState places every entity: the handle must hold no static entities (all_lanes)");
@@ -3941,7 +3953,7 @@ gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* arg
     Params p = g->base;
     p.mode = op; p.obs_lane = lane; p.actions = args; p.comp_out = result; p.obs = obs; p.err = err_flags;
     p.nsteps = 1;
-    HIPCHK(part_launch(g, PK_COMP, g->smem_step, p, (hipStream_t)stream));
+    HIPCHK(part_launch(g, g->wg ? PK_WG_COMP : PK_COMP, g->smem_step, p, (hipStream_t)stream));
     return GW_OK;
 }
 

@@ -7,6 +7,7 @@ ObservingAgent :120-171, Agent :174-186, AgentBasedSimulation :189-294).
 from abc import ABC, abstractmethod
 
 from abmarl_amd import spaces as sp
+from abmarl_amd.sim import host_version
 
 
 class PrincipleAgent:
@@ -41,6 +42,7 @@ class PrincipleAgent:
     def active(self, value):
         assert type(value) is bool, "Active must be either True or False."
         self._active = value
+        host_version.bump()
 
     @property
     def configured(self):

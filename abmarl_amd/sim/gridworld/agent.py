@@ -8,6 +8,7 @@ they are mirrored back onto these objects after every call.
 """
 import numpy as np
 
+from abmarl_amd.sim import host_version
 from abmarl_amd.sim.agent_based_simulation import PrincipleAgent, ActingAgent, ObservingAgent
 
 
@@ -36,6 +37,16 @@ class GridWorldAgent(PrincipleAgent):
         assert value != -1, "-1 encoding reserved for out of bounds."
         assert value != 0, "0 encoding reserved for empty cell."
         self._encoding = value
+
+    @property
+    def position(self):
+        """The agent's position in the grid (agent.py:54-63)."""
+        return self._position
+
+    @position.setter
+    def position(self, value):
+        self._position = value
+        host_version.bump()
 
     @property
     def initial_position(self):

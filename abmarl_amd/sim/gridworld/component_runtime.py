@@ -21,12 +21,21 @@ One runtime per (grid, agents dict); it is rebuilt when the agents'
 attributes or the grid's overlapping change.  The components' own parameters
 (no_overlap_at_reset, stacked_attacks, attack_mapping, observe_self) travel
 with each call, so several actors / observers may share a grid, as in the
-reference's tests.  Limit: the one-wave engine (at most 64 entities).
+reference's tests.  Up to 64 entities run on the one-wave engine, up to
+GW_MAX_LANES (256) on the workgroup-per-env engine (wg_comp_kernel; the
+BASELINE config-4 grid of 256 entities).
+
+Host <-> device traffic per call is kept small: the state is uploaded only
+when the host changed it since the last call (agent / Grid setters bump
+sim/host_version.py; the numpy stream is compared word for word), in-cell
+order goes up as per-cell ranks, and the download rewrites only the Grid
+cells whose occupants moved.
 """
 import numpy as np
 import torch
 
 from abmarl_amd import _abi
+from abmarl_amd.sim import host_version
 from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent
 
 
@@ -46,6 +55,10 @@ def register_component(component):
 
 
 class ComponentRuntime:
+    # run the component ops on the workgroup-per-env engine even for <= 64
+    # entities (tests: both kernels on the reference's component tests)
+    force_workgroup = False
+
     @staticmethod
     def of(component):
         grid, agents = component.grid, component.agents
@@ -58,9 +71,12 @@ class ComponentRuntime:
 
     @staticmethod
     def _signature(grid, agents):
-        from abmarl_amd.sim.gridworld.components import SelectiveAttackActor
+        from abmarl_amd.sim.gridworld.components import SelectiveAttackActor, PositionCenteredEncodingObserver
+        mine = [c for c in _registry(grid) if c.agents is agents]
         sig = [tuple(agents), tuple(sorted(grid.overlap_bits().items())),
-               any(isinstance(c, SelectiveAttackActor) and c.agents is agents for c in _registry(grid))]
+               any(isinstance(c, SelectiveAttackActor) for c in mine),
+               ComponentRuntime.force_workgroup,
+               any(isinstance(c, PositionCenteredEncodingObserver) for c in mine)]
         sig.append(tuple((a.encoding, getattr(a, 'view_range', None), getattr(a, 'move_range', None),
                           getattr(a, 'attack_range', None), getattr(a, 'attack_strength', None),
                           getattr(a, 'attack_accuracy', None), getattr(a, 'simultaneous_attacks', None),
@@ -75,8 +91,8 @@ class ComponentRuntime:
         self.grid, self.agents, self.sig = grid, agents, sig
         self.ids = list(agents)
         self.index = {aid: i for i, aid in enumerate(self.ids)}
-        if len(self.ids) > 64:
-            raise ComponentError("the component runtime holds at most 64 entities per grid")
+        if len(self.ids) > _abi.GW_MAX_LANES:
+            raise ComponentError(f"the component runtime holds at most {_abi.GW_MAX_LANES} entities per grid")
         # selective actions need the (2r+1)^2 action row; binary uses args[2] only
         kind = _abi.GW_ATTACK_SELECTIVE if sig[2] else _abi.GW_ATTACK_BINARY
         # the position-centred window is capped at GW_MAX_RANGE; the absolute
@@ -86,21 +102,39 @@ class ComponentRuntime:
         specs = [agent_spec(a) for a in agents.values()]
         for s_ in specs:
             s_.view_range = min(s_.view_range, _abi.GW_MAX_RANGE)
+            if not sig[4] and s_.kind & _abi.GW_K_GRID_OBSERVER:
+                # no position-centred window on this grid: one view range
+                # (the absolute observer takes its own with each call)
+                s_.view_range = max(views)
         cc = _abi.CompiledConfig(
             grid.rows, grid.cols, specs, _abi.GW_SIM_TEAM_BATTLE,
             grid.overlap_bits(), {}, done_kind=_abi.GW_DONE_ACTIVE,
-            obs_range=max(views) if views else 0, attack_kind=kind)
+            obs_range=max(views) if views else 0, attack_kind=kind,
+            force_workgroup=ComponentRuntime.force_workgroup)
         cc.cfg.all_lanes = 1
         self.cc = cc
-        self.eng = GridWorldEngine(cc, 1, seeds=[0])
+        try:
+            self.eng = GridWorldEngine(cc, 1, seeds=[0])
+        except RuntimeError as err:
+            raise ComponentError(f"the component runtime cannot hold this grid: {err}") from err
         self.dev = self.eng.device
         assert list(self.eng.lane_entities) == list(range(len(self.ids)))
         A = len(self.ids)
         self.result = torch.zeros((1, 2 + A), dtype=torch.int32, device=self.dev)
         self.args = torch.zeros((1, self.eng.act_dim), dtype=torch.int32, device=self.dev)
         self.obs = torch.full((1, A) + self.eng.obs_shape, -2, dtype=torch.int32, device=self.dev)
+        self._healthy = np.array([isinstance(a, HealthAgent) for a in agents.values()])
+        # what the device holds after the last call: host version, numpy
+        # stream, and the entities' (in grid, row, col, seq) for the mirror
+        self._synced = None
+        self._where = None
 
     # ------------------------------------------------------------- sync
+    def _rng_matches(self):
+        st = np.random.get_state()
+        s = self._synced
+        return (st[2] == s[1] and st[3] == s[3] and st[4] == s[4] and np.array_equal(st[1], s[2]))
+
     def _upload(self):
         A = len(self.ids)
         pos = np.zeros((1, A, 2), np.int32)
@@ -108,26 +142,21 @@ class ComponentRuntime:
         flags = np.zeros((1, A), np.uint8)
         seq = np.zeros((1, A), np.int32)
         cells = self.grid._internal
-        order = {}
-        if any(cells[r, c] for r in range(self.grid.rows) for c in range(self.grid.cols)):
-            k = 0
-            for r in range(self.grid.rows):
-                for c in range(self.grid.cols):
-                    for aid in (cells[r, c] or {}):
-                        order[aid] = (k, r, c)
-                        k += 1
         for i, (aid, a) in enumerate(self.agents.items()):
-            if a.position is not None:
-                pos[0, i] = a.position
             f = _abi.FLAG_LIVE
-            if aid in order:
-                seq[0, i] = order[aid][0]
-                pos[0, i] = order[aid][1:]
-                f |= _abi.FLAG_IN_GRID
+            p = a.position
+            if p is not None:
+                pos[0, i] = p
+                cell = cells[int(p[0]), int(p[1])] if 0 <= p[0] < self.grid.rows and 0 <= p[1] < self.grid.cols \
+                    else None
+                if cell and aid in cell:
+                    # in-cell insertion order as the rank inside the cell
+                    seq[0, i] = list(cell).index(aid)
+                    f |= _abi.FLAG_IN_GRID
             if a.active:
                 f |= _abi.FLAG_ACTIVE
             flags[0, i] = f
-            if isinstance(a, HealthAgent) and a.health is not None:
+            if self._healthy[i] and a.health is not None:
                 health[0, i] = a.health
         st = np.random.get_state()
         assert st[0] == 'MT19937'
@@ -135,40 +164,53 @@ class ComponentRuntime:
         mt = np.zeros((1, _abi.GW_MT_STRIDE), np.uint32)
         mt[0, :624] = st[1]
         mt[0, 624] = st[2]
-        mt[0, 625] = A                      # next placement sequence number
+        mt[0, 625] = A                      # next placement sequence number (> every rank)
         d = self.dev
         self.eng.set_state(pos=torch.as_tensor(pos, device=d), health=torch.as_tensor(health, device=d),
                            flags=torch.as_tensor(flags, device=d), seq=torch.as_tensor(seq, device=d),
                            mt=torch.as_tensor(mt.view(np.int32), device=d))
+        self._where = (flags[0] & _abi.FLAG_IN_GRID != 0, pos[0].copy(), seq[0].copy())
 
     def _download(self, op):
         st = {k: v.cpu().numpy() for k, v in self.eng.get_state().items()}
         mt = st['mt'].view(np.uint32)[0]
         np.random.set_state(('MT19937', mt[:624].copy(), int(mt[624])) + tuple(self._gauss))
         flags = st['flags'][0]
-        in_grid = []
-        for i, (aid, a) in enumerate(self.agents.items()):
-            inside = bool(flags[i] & _abi.FLAG_IN_GRID)
-            if inside or a.position is not None:
-                a.position = st['pos'][0, i].astype(int)
-            if isinstance(a, HealthAgent) and (a.health is not None or op == _abi.GW_OP_HEALTH_RESET):
-                a._health = float(st['health'][0, i])
+        inside = (flags & _abi.FLAG_IN_GRID) != 0
+        pos, seq, health = st['pos'][0], st['seq'][0], st['health'][0]
+        agents = list(self.agents.values())
+        for i, a in enumerate(agents):
+            if inside[i] or a.position is not None:
+                a._position = pos[i].astype(int)
+            if self._healthy[i] and (a.health is not None or op == _abi.GW_OP_HEALTH_RESET):
+                a._health = float(health[i])
             a._active = bool(flags[i] & _abi.FLAG_ACTIVE)
-            if inside:
-                in_grid.append((int(st['seq'][0, i]), aid, a))
         cells = self.grid._internal
-        if op in (_abi.GW_OP_POSITION_RESET, _abi.GW_OP_MAZE_RESET) or any(cells[r, c] is not None for r in range(self.grid.rows)
-                         for c in range(self.grid.cols)):
-            self.grid.reset()
-            for _, aid, a in sorted(in_grid, key=lambda x: x[0]):
-                cells[tuple(a.position)][aid] = a
+        old_in, old_pos, old_seq = self._where
+        moved = (inside != old_in) | (inside & ((pos != old_pos).any(1) | (seq != old_seq)))
+        if op in (_abi.GW_OP_POSITION_RESET, _abi.GW_OP_MAZE_RESET) or cells[0, 0] is None:
+            for r in range(self.grid.rows):
+                for c in range(self.grid.cols):
+                    cells[r, c] = {}
+            touched = {(int(p[0]), int(p[1])) for p in pos[inside]}
+        else:
+            touched = {(int(p[0]), int(p[1])) for p in old_pos[moved & old_in]} | \
+                      {(int(p[0]), int(p[1])) for p in pos[moved & inside]}
+        # each touched cell: its occupants in insertion (seq) order
+        for rc in touched:
+            here = np.nonzero(inside & (pos[:, 0] == rc[0]) & (pos[:, 1] == rc[1]))[0]
+            cells[rc] = {self.ids[i]: agents[i] for i in here[np.argsort(seq[here], kind='stable')]}
+        self._where = (inside, pos.copy(), seq.copy())
+        s = np.random.get_state()
+        self._synced = (host_version.VERSION[0], s[2], s[1].copy(), s[3], s[4])
 
     # ----------------------------------------------------------- operations
     def op(self, op, agent=None, args=None):
         """Run one component operation; returns (status, attacked agents, err)
         (the raw result row stays in self.last_result)."""
         lane = -1 if agent is None else self.index[agent.id]
-        self._upload()
+        if self._synced is None or self._synced[0] != host_version.VERSION[0] or not self._rng_matches():
+            self._upload()
         if args is not None:
             a = np.zeros((1, self.eng.act_dim), np.int32)
             flat = np.asarray(args, dtype=np.int64).reshape(-1)
@@ -180,7 +222,8 @@ class ComponentRuntime:
         res = self.last_result = self.result[0].cpu().numpy()
         err = int(self.eng.err[0].item())
         self._download(op)
-        attacked = [self.agents[self.ids[int(x)]] for x in res[2:2 + int(res[1])]]
+        attacked = [self.agents[self.ids[int(x)]] for x in res[2:2 + int(res[1])]] \
+            if op == _abi.GW_OP_ATTACK else []
         return int(res[0]), attacked, err
 
     def _abs_obs(self):

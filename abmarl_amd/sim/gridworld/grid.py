@@ -15,6 +15,8 @@ import copy
 
 import numpy as np
 
+from abmarl_amd.sim import host_version
+
 
 class Grid:
     def __init__(self, rows, cols, overlapping=None, **kwargs):
@@ -66,6 +68,7 @@ class Grid:
         for i in range(self.rows):
             for j in range(self.cols):
                 self._internal[i, j] = {}
+        host_version.bump()
 
     def query(self, agent, ndx):
         """The cell is empty, or every occupant's encoding may overlap this
@@ -85,12 +88,14 @@ class Grid:
         if self.query(agent, ndx):
             self._internal[ndx][agent.id] = agent
             agent.position = np.array(ndx)
+            host_version.bump()
             return True
         return False
 
     def remove(self, agent, ndx):
         """grid.py:131-140 (KeyError if the agent is not in the cell)."""
         del self._internal[tuple(ndx)][agent.id]
+        host_version.bump()
 
     def __getitem__(self, subscript):
         return self._internal.__getitem__(subscript)

@@ -39,8 +39,9 @@ def build_maze(c):
         states={'PositionState'}, observers={'PositionCenteredEncodingObserver'})
 
 
-def build_rtt(c):
-    """ReachTheTarget as in the reference's examples/rllib_reach_the_target.py."""
+def build_rtt(c, sim_cls=None):
+    """ReachTheTarget as in the reference's examples/rllib_reach_the_target.py
+    (sim_cls: a user-written simulation class instead of the program's)."""
     R, C = c['rows'], c['cols']
     corners = [[0, 0], [R - 1, 0], [0, C - 1], [R - 1, C - 1]]
     agents = {f'barrier{i}': BarrierAgent(id=f'barrier{i}') for i in range(c['n_barriers'])}
@@ -55,7 +56,7 @@ def build_rtt(c):
     agents['target'] = TargetAgent(**kw)
     ov = {int(k): set(v) for k, v in c['overlapping'].items()} if 'overlapping' in c \
         else {2: {3}, 3: {1, 2, 3}}
-    return ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping=ov, attack_mapping={2: {3}})
+    return (sim_cls or ReachTheTargetSim).build_sim(R, C, agents=agents, overlapping=ov, attack_mapping={2: {3}})
 
 
 # BASELINE config 4: ReachTheTarget 64x64, 128 barriers + 127 runners + the
@@ -97,7 +98,7 @@ def build_sim(c, sim_cls=None):
     if c.get('kind') == 'traffic':
         return build_traffic(c)
     if c.get('kind') == 'rtt':
-        return build_rtt(c)
+        return build_rtt(c, sim_cls)
     agents = {}
     for i in range(c['n_agents']):
         kw = dict(id=f'agent{i}', encoding=i % c['n_teams'] + 1, **c['agent'])

@@ -33,6 +33,25 @@ gpu = pytest.mark.gpu
 KEY = 'position_centered_encoding'
 
 
+@pytest.fixture(params=['wave', 'workgroup'], autouse=True)
+def component_kernel(request):
+    """Every GPU test of this module on both component kernels: the one-wave
+    comp_kernel and the workgroup-per-env wg_comp_kernel (forced below its
+    usual > 64-entity threshold)."""
+    from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
+    if request.param == 'workgroup':
+        if request.node.get_closest_marker('gpu') is None:
+            pytest.skip('CPU test: one kernel')
+        if 'tb_views' in request.node.name or 'position_centered_observer' in request.node.name or \
+                'observe_self' in request.node.name:
+            pytest.skip('observers with different view ranges: the one-wave kernel only')
+        if 'randomize_placement_order' in request.node.name or 'tb_order' in request.node.name:
+            pytest.skip('randomize_placement_order / placement orders: the one-wave kernel only')
+    ComponentRuntime.force_workgroup = request.param == 'workgroup'
+    yield request.param
+    ComponentRuntime.force_workgroup = False
+
+
 # ------------------------------------------------------------------ states
 @gpu
 def test_position_state_randomize_placement_order():
@@ -500,6 +519,136 @@ def test_user_step_replays_reference(name, steps, envs):
                 obs = m.reset()
                 np.testing.assert_array_equal(_obs_array(obs, ids, S), g['reset_obs'][t, e],
                                               err_msg=where + ' reset')
+
+
+# ------------------------------ ReachTheTarget, BASELINE config 4, user step
+def _user_rtt_class():
+    """Test-side user code: the reference's ReachTheTarget example
+    (examples/sim/reach_the_target.py:84-158) written against this
+    repository's components, dones as plain reads of the agents."""
+    from abmarl_amd.sim.agent_based_simulation import Agent
+    from abmarl_amd.sim.gridworld.base import GridWorldSimulation
+    from abmarl_amd.examples.reach_the_target import RunningAgent, TargetAgent
+
+    class UserReachTheTarget(GridWorldSimulation):
+        def __init__(self, **kw):
+            super().__init__(**kw)
+            self.target = self.agents['target']
+            self.position_state = PositionState(**kw)
+            self.health_state = HealthState(**kw)
+            self.move_actor = MoveActor(**kw)
+            self.attack_actor = SelectiveAttackActor(**kw)
+            self.observer = PositionCenteredEncodingObserver(**kw)
+            self.finalize()
+
+        def reset(self, **kw):
+            self.health_state.reset(**kw)
+            self.position_state.reset(**kw)
+            self.rewards = {a.id: 0 for a in self.agents.values() if isinstance(a, Agent)}
+
+        def _on_target(self, agent):
+            return agent is not self.target and np.array_equal(agent.position, self.target.position)
+
+        def _left(self):
+            return sum(1 for a in self.agents.values() if a.active and isinstance(a, Agent))
+
+        def step(self, action_dict, **kw):
+            for aid, action in action_dict.items():
+                agent = self.agents[aid]
+                if not agent.active:
+                    continue
+                status, hit = self.attack_actor.process_action(agent, action, **kw)
+                if status and not hit:
+                    self.rewards[aid] -= 0.1
+                for other in hit:
+                    if not other.active:
+                        self.rewards[other.id] -= 1
+                        self.rewards[aid] += 1
+            for aid, action in action_dict.items():
+                agent = self.agents[aid]
+                if not isinstance(agent, MovingAgent):
+                    continue
+                if agent.active and not self.move_actor.process_action(agent, action, **kw):
+                    self.rewards[aid] -= 0.1
+                if self._on_target(agent):
+                    self.rewards[aid] += 1
+                    self.grid.remove(agent, agent.position)
+                    agent.active = False
+            for aid in action_dict:
+                if isinstance(self.agents[aid], RunningAgent):
+                    self.rewards[aid] -= 0.01
+
+        def get_obs(self, aid, **kw):
+            return dict(self.observer.get_obs(self.agents[aid], **kw))
+
+        def get_reward(self, aid, **kw):
+            r, self.rewards[aid] = self.rewards[aid], 0
+            return r
+
+        def get_done(self, aid, **kw):
+            agent = self.agents[aid]
+            if isinstance(agent, RunningAgent):
+                return not agent.active or self._on_target(agent)
+            if isinstance(agent, TargetAgent):
+                return self._left() <= 1
+
+        def get_all_done(self, **kw):
+            return self._left() <= 1
+
+        def get_info(self, aid, **kw):
+            return {}
+
+    return UserReachTheTarget
+
+
+@gpu
+def test_user_rtt_config4_replays_reference(component_kernel):
+    """BASELINE config 4's grid (64x64, 128 barriers + 127 runners + the
+    target = 256 entities: the workgroup-per-env component kernel) driven
+    by a user-written step() through MultiAgentWrapper(AllStepManager), one
+    component call at a time, against the reference's own trajectory
+    (tests/golden/rtt_64.npz): observations, reward bits, dones, positions,
+    health and the numpy stream after every step."""
+    if component_kernel != 'wave':
+        pytest.skip('256 entities always run on the workgroup kernel')
+    from abmarl_amd.external import MultiAgentWrapper
+    from abmarl_amd.sim.agent_based_simulation import Agent
+    from tests.cases import load_golden, build_rtt
+    from tests.test_dict_api import _check_obs, _action
+    g = load_golden('rtt_64')
+    c = g['case']
+    steps = 12
+    for e in range(2):
+        sim = build_rtt(c, sim_cls=_user_rtt_class())
+        ids = list(sim.agents)
+        index = {k: i for i, k in enumerate(ids)}
+        agents0 = np.array([isinstance(a, Agent) for a in sim.agents.values()])
+        env = MultiAgentWrapper(AllStepManager(sim))
+        np.random.seed(c['seeds'][e])
+        obs = env.reset()
+        from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
+        rt = ComponentRuntime.of(sim.observer)
+        assert rt.eng.wg and len(rt.ids) == 256
+        _check_obs(obs, g['obs0'][e], agents0, index)
+        for t in range(steps):
+            done_agents = env.sim.done_agents
+            adict = {k: _action(sim.agents[k], g['actions'][t, e, i])
+                     for i, k in enumerate(ids) if k not in done_agents}
+            assert not g['err'][t, e]
+            o, r, d, _ = env.step(adict)
+            _check_obs(o, g['obs'][t, e], g['returned'][t, e], index)
+            for k, v in r.items():
+                i = index[k]
+                assert np.float64(v).view(np.uint64) == g['reward'][t, e, i].view(np.uint64), (t, k)
+                assert bool(d[k]) == bool(g['done'][t, e, i]), (t, k)
+            assert bool(d['__all__']) == bool(g['all_done'][t, e])
+            st = np.random.get_state()
+            assert st[2] == g['mt_pos'][t, e]
+            assert zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes()) == g['mt_crc'][t, e]
+            for i, agent in enumerate(sim.agents.values()):
+                np.testing.assert_array_equal(agent.position, g['pos'][t, e, i])
+                assert getattr(agent, 'health', 0.0) == g['health'][t, e, i]
+            assert not g['reset_mask'][t, e]
 
 
 # -------------------------------------------------------------------- CPU

@@ -20,6 +20,16 @@ gpu = pytest.mark.gpu
 ABS = 'absolute_encoding'
 
 
+@pytest.fixture(params=['wave', 'workgroup'], autouse=True)
+def component_kernel(request):
+    """Every test on both component kernels (one-wave comp_kernel, and the
+    workgroup-per-env wg_comp_kernel forced below its > 64-entity threshold)."""
+    from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
+    ComponentRuntime.force_workgroup = request.param == 'workgroup'
+    yield request.param
+    ComponentRuntime.force_workgroup = False
+
+
 def _movers(spec):
     return {aid: MovingAgent(id=aid, initial_position=np.array(p), encoding=enc, move_range=mr)
             for aid, (p, enc, mr) in spec.items()}
@@ -225,6 +235,31 @@ def test_absolute_encoding_observer_view_beyond_window_cap():
         want = _host_absolute(agents['eye'], grid, agents)
         np.testing.assert_array_equal(got, want)
         assert rng is not None
+
+
+@gpu
+def test_absolute_encoding_observer_256_entities():
+    """The workgroup kernel at its full width: 256 entities on a 40x40 grid
+    (blockers, crowded cells), several observers, against the host
+    restatement with the same numpy stream."""
+    grid = Grid(40, 40, overlapping={1: {2}, 2: {1, 2}})
+    agents = {f'eye{i}': GridObservingAgent(id=f'eye{i}', encoding=1, view_range=v)
+              for i, v in enumerate([3, 9, 40, 17])}
+    for i in range(200):
+        agents[f'm{i}'] = GridWorldAgent(id=f'm{i}', encoding=2)
+    for i in range(52):
+        agents[f'w{i}'] = GridWorldAgent(id=f'w{i}', encoding=3, blocking=True)
+    position_state = PositionState(grid=grid, agents=agents)
+    observer = AbsoluteEncodingObserver(agents=agents, grid=grid)
+    np.random.seed(7)
+    position_state.reset()
+    for i in range(4):
+        eye = agents[f'eye{i}']
+        st = np.random.get_state()
+        got = observer.get_obs(eye)[ABS]
+        np.random.set_state(st)
+        want = _host_absolute(eye, grid, agents)
+        np.testing.assert_array_equal(got, want, err_msg=f'eye{i}')
 
 
 def _host_absolute(agent, grid, agents):

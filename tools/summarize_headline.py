@@ -110,7 +110,7 @@ def main():
                                        'SGPR_Count', 'Workgroup_Size_X', 'Grid_Size_X') if k in rows[timed]}
     # PMC passes (the short command: the first engine's run only)
     p = {}
-    for d in sorted(glob.glob(os.path.join(a.raw, 'p*'))):
+    for d in sorted(glob.glob(os.path.join(a.raw, 'p[0-9]*'))):
         if os.path.isdir(d):
             for k, v in counters(d).items():
                 p[k] = v
