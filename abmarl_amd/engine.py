@@ -398,6 +398,33 @@ class GridWorldEngine:
         self._check_debug('gw_rollout')
         return out
 
+    def rollout_launcher(self, actions, horizon=0, autoreset='next_step', skip_done_obs=False, out=None):
+        """A prepared gw_rollout launch: the arguments of rollout(actions, ...)
+        are validated and built once, on the current stream, and the returned
+        zero-argument callable launches exactly that fragment with one ctypes
+        call (a training loop re-launching the same slabs, or a benchmark's
+        timed region).  It keeps references to `actions` and `out`."""
+        K = int(actions.shape[0])
+        assert actions.dtype == torch.int32 and actions.is_contiguous()
+        assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
+        assert autoreset in ('same_step', 'next_step'), autoreset
+        assert actions.device == self.device, (actions.device, self.device)
+        assert torch.cuda.current_device() == self.device.index, "launcher: the engine's device must be current"
+        out = self.rollout_buffers(K) if out is None else out
+        self._check_rollout_buffers(K, out)
+        fn, h = self.L.gw_rollout, self.h
+        args = (h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
+                self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream())
+        keep = (actions, out)
+
+        def launch():
+            st = fn(*args)
+            if st != 0:
+                _native.check(st, 'gw_rollout')
+            return keep[1]
+        return launch
+
     def rollout_step(self, key, step, env_offset=0, horizon=0, autoreset='next_step'):
         """One synthetic random-policy rollout step in ONE C-ABI call
         (gw_rollout_step: Philox actions into self.actions, then the step with

@@ -413,21 +413,22 @@ def main():
     def run_rollout(eng, mode):
         """Pre-roll and warmup as rollout fragments, then the K timed steps as
         gw_rollout fragments of up to --fragment steps on actions generated
-        into HBM before the timed region; HIP events around every launch."""
+        into HBM before the timed region; HIP events around every launch.
+
+        The GPU works until the synchronize that opens the timed region: the
+        timed steps' actions and the acting-counter snapshot are produced
+        before the last warmup fragment / right after it, on the device, so
+        no host round trip leaves the GPU idle between the warmup and t0."""
         F = max(1, min(args.fragment, args.steps))
         nfrag = max(F, min(args.fragment, max(untimed, 1)))
-        # ONE action buffer for the pre-roll, the warmup and the timed steps
-        # (a training loop reuses its buffers): the timed fragments read
-        # pages the untimed ones already used, not a fresh allocation whose
-        # first launch pays cold address translation (tools/first_launch_probe2.py)
-        acts_all = torch.empty((max(nfrag, args.steps),) + tuple(eng.actions.shape),
+        # warmup actions [0, nfrag), timed actions [nfrag, nfrag + steps)
+        acts_all = torch.empty((nfrag + args.steps,) + tuple(eng.actions.shape),
                                dtype=torch.int32, device=eng.device)
         acts = acts_all[:nfrag]
         out = eng.rollout_buffers(nfrag)
         # untimed pre-roll + warmup as fragments of up to nfrag steps, the
         # last one exactly F steps: it writes the same output slabs and reads
-        # the same action slabs as the timed fragments, so the timed launch
-        # does not start on cold address translations for them
+        # actions laid out as the timed fragments'
         sizes, rest = [], untimed
         last = min(F, rest)
         rest -= last
@@ -436,41 +437,48 @@ def main():
             rest -= sizes[-1]
         if last:
             sizes.append(last)
+        all_acts = acts_all[nfrag:nfrag + args.steps]
+        frags = [(i, min(F, args.steps - i)) for i in range(0, args.steps, F)]
+        if not sizes:
+            for s in range(args.steps):
+                eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
         t = 0
-        for f in sizes:
+        for k, f in enumerate(sizes):
             for s in range(f):
                 eng.random_actions(key, t + s, env_offset=first, out=acts[s])
+            if k == len(sizes) - 1:
+                # the timed steps' actions (inputs resident in HBM before timing)
+                for s in range(args.steps):
+                    eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
             eng.rollout(acts[:f], horizon=args.horizon, autoreset=mode, skip_done_obs=True, out=out)
             t += f
-        torch.cuda.synchronize()
-        eng.check_errors(allow=allow)
-        # the timed steps' actions: inputs resident in HBM before timing
-        all_acts = acts_all[:args.steps]
-        for s in range(args.steps):
-            eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
-        frags = [(i, min(F, args.steps - i)) for i in range(0, args.steps, F)]
+            if k == len(sizes) - 2:
+                torch.cuda.synchronize()
+                eng.check_errors(allow=allow)
+        # prepared launches (validated here, one ctypes call each when timed)
+        # and their events, created by a first record outside the timed region
+        launches = [eng.rollout_launcher(all_acts[i:i + f], horizon=args.horizon, autoreset=mode,
+                                         skip_done_obs=True, out=out) for i, f in frags]
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in frags]
-        torch.cuda.synchronize()
-        acting0 = int(eng.acting.sum().item())
+        for a_, b_ in evs:
+            a_.record()
+            b_.record()
+        acting0 = eng.acting.clone()                      # after the last warmup fragment
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        host_ms = []
-        for (i, f), ev in zip(frags, evs):
-            h0 = time.perf_counter()
+        for launch, ev in zip(launches, evs):
             ev[0].record()
-            eng.rollout(all_acts[i:i + f], horizon=args.horizon, autoreset=mode, skip_done_obs=True,
-                        out=out)
+            launch()
             ev[1].record()
-            host_ms.append((time.perf_counter() - h0) * 1e3)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         dt = time.perf_counter() - t0
         eng.check_errors(allow=allow)
-        acting = int(eng.acting.sum().item()) - acting0
+        acting = int((eng.acting - acting0).sum().item())
         # launch-weighted mean: ms per launch of the full-size fragments
         full = [a.elapsed_time(b) for (i, f), (a, b) in zip(frags, evs) if f == F]
         launch_ms = float(np.mean(full))
@@ -483,7 +491,7 @@ def main():
             tot = torch.stack([acts_t[0], tmax[1], acts_t[2]])
         return dict(acting=tot[0].item(), dt=tot[1].item(), envs=tot[2].item(),
                     step_ms=launch_ms, step_ms_max=kms[0].item(), steps_per_launch=F,
-                    acting_local=acting, host_launch_ms=float(np.mean(host_ms)))
+                    acting_local=acting)
 
     mode = 'next_step' if turn else args.autoreset
     rollout = args.mode == 'rollout' and not turn
@@ -571,7 +579,6 @@ def main():
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
             'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
             'acting_agent_steps': int(acting_all),
-            'host_launch_ms': (round(r['host_launch_ms'], 4) if 'host_launch_ms' in r else None),
             'roofline': roof,
             'episode_stats': stats,
             'autoreset': mode,

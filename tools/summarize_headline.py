@@ -158,7 +158,7 @@ def main():
           f'- idle gap before the timed launch (after `{prev_name}` ended): {gap:.1f} us '
           '(host: synchronize, acting read-back, synchronize, event record, launch)',
           f'- the same run\'s HIP-event launch time (bench line `roofline.kernel_ms`): '
-          f'{roof.get("kernel_ms")} ms; host time of the launch call: {line.get("host_launch_ms")} ms; '
+          f'{roof.get("kernel_ms")} ms; '
           f'wall ms_per_step x 20: {line.get("ms_per_step", 0) * 20:.4f} ms; value {line.get("value"):.4g}',
           f'- resources: `{res}`', '',
           '## Traffic of the timed launch (PMC run)', '',
