@@ -48,6 +48,7 @@ GW_K_PROGRAM = 0x80
 GW_K_BLOCKING = 0x40
 GW_K_ORIENTATION = 0x100
 GW_K_FOOD = 0x200
+GW_K_LANE = 0x400
 
 GW_SIM_TEAM_BATTLE = 1
 GW_SIM_MAZE_NAV = 2
@@ -129,6 +130,7 @@ class Config(C.Structure):
         ("persistent_obs", C.c_int32),
         ("all_lanes", C.c_int32),
         ("env_per_lane", C.c_int32),
+        ("component_api", C.c_int32),
     ]
 
 

@@ -61,7 +61,11 @@
 #define CELL_OFF 0xFFu
 // lane_step_kernel (gw_lane.inc): lanes per env for an S x S window (the
 // window's cell count rounded up to 16, 32 or 64; host and device)
+#ifdef GW_LANE_GROUP
+__host__ __device__ constexpr int lane_group(int) { return GW_LANE_GROUP; }
+#else
 __host__ __device__ constexpr int lane_group(int S) { return S * S <= 16 ? 16 : (S * S <= 32 ? 32 : 64); }
+#endif
 
 // create_grid_and_mask (utils.py:46-115): does a blocker at offset (rd, cd)
 // from the observer hide the cell at offset (r, c)?  The eight cases differ
@@ -3125,7 +3129,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     for (int a = 0; a < NE; a++) {
         const gw_agent_spec& s = cfg->agents[a];
         if (pac && (s.kind & GW_K_FOOD)) { passive.push_back(a); continue; }
-        const bool st = !cfg->all_lanes && !(s.kind & dynamic_kinds) && s.init_row >= 0 && s.init_col >= 0 &&
+        const bool st = !cfg->all_lanes && !(s.kind & (dynamic_kinds | GW_K_LANE)) && s.init_row >= 0 && s.init_col >= 0 &&
                         cfg->overlap[s.encoding] == 0 && !((overlapped >> s.encoding) & 1u) &&
                         !((attacked >> s.encoding) & 1u) &&
                         !((maze || rtt) && (a == cfg->nav_agent || a == cfg->target_agent));
@@ -3140,11 +3144,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // when the config forces it: the parity tests run small reference
     // fixtures through it)
     const bool tb = cfg->sim_kind == GW_SIM_TEAM_BATTLE;
-    // (a component-API handle, every entity a lane, runs only gw_component
-    // operations: either attack kind)
+    // (a component-API handle runs only gw_component operations: either
+    // attack kind)
     const bool wg_able = (rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE) ||
                          (tb && cfg->attack_kind == GW_ATTACK_BINARY) ||
-                         (cfg->all_lanes && (rtt || tb));
+                         (cfg->component_api && (rtt || tb));
     if (cfg->force_workgroup && !wg_able) {
         set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor "
                 "and TeamBattle with BinaryAttackActor");

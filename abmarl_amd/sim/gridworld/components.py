@@ -63,7 +63,7 @@ class PositionState(StateBaseComponent):
             # for the next reset (Python's own random: the reference's draws)
             items = self.__dict__.setdefault('_place_items', list(self.agents))
             random.shuffle(items)
-            rt.eng.set_placement_order([rt.index[aid] for aid in items])
+            rt.eng.set_placement_order([rt.index[aid] for aid in items if aid in rt.index])
         status, _, err = rt.op(_abi.GW_OP_POSITION_RESET, args=[int(self.no_overlap_at_reset)])
         if err & _abi.GW_ERR_INIT_POSITION:
             raise AssertionError("Cell is not available for an agent with an initial position.")
@@ -151,7 +151,7 @@ class _TargetPlacementState(PositionState):
         if self.randomize_placement_order:
             items = self.__dict__.setdefault('_place_items', list(self.agents))
             random.shuffle(items)
-            rt.eng.set_placement_order([rt.index[aid] for aid in items])
+            rt.eng.set_placement_order([rt.index[aid] for aid in items if aid in rt.index])
         for agent in self.agents.values():
             assert agent.encoding in {*self.barrier_encodings, *self.free_encodings}, \
                 "All agent encodings must be either barrier or free cell."

@@ -116,6 +116,9 @@ typedef int32_t gw_status;
 #define GW_K_ORIENTATION  0x100u /* OrientationAgent          gridworld/agent.py:342-373   */
 #define GW_K_FOOD         0x200u /* Pacman FoodAgent (pacman.py:17-19); with GW_SIM_PACMAN,
                                     GW_K_PROGRAM marks its BaddieAgent (pacman.py:22-24) */
+#define GW_K_LANE         0x400u /* never a static entity: the caller may read or edit
+                                    it (the component runtime keeps blocking entities
+                                    as lanes: the absolute observer's masks take lanes) */
 #define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75;
                                     active blocking entities mask cells from
                                     observers and attackers (utils.py:5-117) */
@@ -215,6 +218,9 @@ typedef struct gw_config {
        (gw_create fails if the config is not eligible), -1 = never (one
        wavefront per env)                                                     */
     int32_t  env_per_lane;
+    /* 1: a component-API handle (gw_component only, no step program): either
+       attack kind on the workgroup-per-env engine above 64 lanes           */
+    int32_t  component_api;
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack

@@ -628,7 +628,7 @@ def test_user_rtt_config4_replays_reference(component_kernel):
         obs = env.reset()
         from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
         rt = ComponentRuntime.of(sim.observer)
-        assert rt.eng.wg and len(rt.ids) == 256
+        assert rt.eng.wg and len(rt.lane_ids) == 256
         _check_obs(obs, g['obs0'][e], agents0, index)
         for t in range(steps):
             done_agents = env.sim.done_agents

@@ -286,3 +286,133 @@ def _host_absolute(agent, grid, agents):
             else:
                 obs[gr, gc] = np.random.choice([o.encoding for o in cell.values()])
     return obs
+
+
+# --------------------------- Pacman (BASELINE config 5's map), user step
+def _user_pacman_class():
+    """Test-side user code: the reference's PacmanSim (examples/sim/pacman.py:
+    29-153) written against this repository's components -- DriftMoveActor
+    moves, OrientationState / PositionState / HealthState resets and the
+    AbsoluteEncodingObserver on the device, the tunnel and the overlaps as
+    host Grid edits between the calls."""
+    from abmarl_amd.sim.gridworld.smart import SmartGridWorldSimulation
+    from abmarl_amd.examples.pacman import FoodAgent, BaddieAgent
+
+    class UserPacman(SmartGridWorldSimulation):
+        def __init__(self, reward_scheme=None, **kw):
+            super().__init__(**kw)
+            self.pacman = self.agents['pacman']
+            self.move_actor = DriftMoveActor(**kw)
+            self.scheme = reward_scheme or {'bad_move': -0.1, 'entropy': 0.01, 'eat_food': 0.1,
+                                            'kill': 1, 'die': -1}
+            self.finalize()
+
+        def _moved(self, aid, ok):
+            self.rewards[aid] += self.scheme['entropy'] if ok else self.scheme['bad_move']
+
+        def _tunnel(self, agent):
+            for a, b in (((9, 0), (9, 20)), ((9, 20), (9, 0))):
+                if np.array_equal(agent.position, np.array(a)):
+                    self.grid.remove(agent, a)
+                    self.grid.place(agent, b)
+                    return
+
+        def _baddies_on_pacman(self, with_food):
+            here = self.grid[self.pacman.position[0], self.pacman.position[1]]
+            for other in here.copy().values():
+                if other.id == self.pacman.id:
+                    continue
+                if with_food and isinstance(other, FoodAgent):
+                    self.rewards['pacman'] += self.scheme['eat_food']
+                    self.grid.remove(other, tuple(self.pacman.position))
+                    other.health = 0
+                elif isinstance(other, BaddieAgent):
+                    self.rewards['pacman'] += self.scheme['die']
+                    self.rewards[other.id] += self.scheme['kill']
+                    self.pacman.health = 0
+
+        def step(self, action_dict, **kw):
+            self._moved('pacman', self.move_actor.process_action(self.pacman, action_dict['pacman'], **kw))
+            self._tunnel(self.pacman)
+            self._baddies_on_pacman(True)
+            for aid, action in action_dict.items():
+                if aid == 'pacman':
+                    continue
+                agent = self.agents[aid]
+                self._moved(aid, self.move_actor.process_action(agent, action, **kw))
+                self._tunnel(agent)
+            self._baddies_on_pacman(False)
+            if not self.pacman.active:
+                self.grid.remove(self.pacman, tuple(self.pacman.position))
+
+        def get_done(self, agent_id, **kw):
+            return self.get_all_done()
+
+        def get_all_done(self, **kw):
+            if not self.pacman.active:
+                return True
+            return not any(isinstance(a, FoodAgent) for a in self.agents.values())
+
+    return UserPacman
+
+
+@gpu
+def test_user_pacman_replays_reference(component_kernel):
+    """The reference's own Pacman trajectories (tests/golden/pacman_4.npz,
+    BASELINE config 5's map: 199 walls, 147 food, pacman, 4 baddies) replayed
+    by the user-written step() above under AllStepManager: the walls stay in
+    the engine's cell template, the other 152 entities run on the
+    workgroup-per-env component kernel.  Observations, reward bits, dones and
+    the numpy stream after every step."""
+    import json
+    import os
+    import zlib
+    from abmarl_amd.managers import AllStepManager
+    from abmarl_amd.examples.pacman import pacman_grid, object_registry
+    from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
+    if component_kernel != 'wave':
+        pytest.skip('152 lanes always run on the workgroup kernel')
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'pacman_4.npz')
+    z = np.load(path, allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    c = json.loads(str(g['case']))
+    cls = _user_pacman_class()
+    steps = 60
+    for e in range(2):
+        sim = cls.build_sim_from_array(
+            pacman_grid(c['baddies']), object_registry(),
+            states={'PositionState', 'OrientationState', 'HealthState'},
+            observers={'AbsoluteEncodingObserver'},
+            overlapping={1: {3, 4}, 4: {3, 4}}, reward_scheme=c['reward_scheme'])
+        assert sim._engine_program is None
+        ids = list(sim.agents)
+        agents = [ids[i] for i in c['agent_index']]
+        m = AllStepManager(sim)
+        np.random.seed(c['seeds'][e])
+        o = m.reset()
+        rt = ComponentRuntime.of(sim.move_actor)
+        assert rt.eng.wg and len(rt.lane_ids) == 152 and len(rt.statics) == 199
+        for j, aid in enumerate(agents):
+            np.testing.assert_array_equal(o[aid][ABS], g['obs0'][e, j], err_msg=f'env {e} reset {aid}')
+        for t in range(steps):
+            adict = {aid: {'move': int(g['actions'][t, e, j])} for j, aid in enumerate(agents)
+                     if aid not in m.done_agents}
+            o, r, d, _ = m.step(adict)
+            where = f'env {e} step {t}'
+            for j, aid in enumerate(agents):
+                if g['returned'][t, e, j]:
+                    np.testing.assert_array_equal(o[aid][ABS], g['obs'][t, e, j], err_msg=f'{where} {aid}')
+                    assert np.float64(r[aid]).view(np.uint64) == \
+                        np.float64(g['reward'][t, e, j]).view(np.uint64), (where, aid)
+                    assert d[aid] == bool(g['done'][t, e, j]), (where, aid)
+            assert d['__all__'] == bool(g['all_done'][t, e]), where
+            st = np.random.get_state()
+            assert st[2] == g['mt_pos'][t, e], where
+            assert zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes()) == g['mt_crc'][t, e], where
+            for j, aid in enumerate(agents):
+                np.testing.assert_array_equal(sim.agents[aid].position, g['pos'][t, e, j], err_msg=where)
+                assert sim.agents[aid].orientation == g['orient'][t, e, j], (where, aid)
+            if g['reset_mask'][t, e]:
+                o = m.reset()
+                for j, aid in enumerate(agents):
+                    np.testing.assert_array_equal(o[aid][ABS], g['reset_obs'][t, e, j], err_msg=where)
