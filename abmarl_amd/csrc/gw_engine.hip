@@ -233,6 +233,33 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, int l) { return __builtin_amd
 __device__ __forceinline__ int32_t rl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ bool rlb(bool v, int l) { return __builtin_amdgcn_readlane((int)v, l) != 0; }
 
+// raw buffer resource word 3 for gfx9 (data format 32, no swizzle, no stride)
+#define BUF_RSRC_W3 0x00020000
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// four observation bytes (valid values >= -2, 0x80 = skipped) -> four int32
+// max(sext(byte), -2) with SDWA byte selects (one VALU per output), stored
+// as one dwordx4 at voff + ioff of the buffer (voff out of range = dropped)
+__device__ __forceinline__ void buf_store_i8x4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int ioff, uint32_t w)
+{
+    const int m2 = -2;
+    int v0, v1, v2, v3;
+    asm("v_max_i32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(v0) : "v"(w), "v"(m2));
+    asm("v_max_i32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(v1) : "v"(w), "v"(m2));
+    asm("v_max_i32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(v2) : "v"(w), "v"(m2));
+    asm("v_max_i32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+        : "=v"(v3) : "v"(w), "v"(m2));
+    const u32x4 v = {(uint32_t)v0, (uint32_t)v1, (uint32_t)v2, (uint32_t)v3};
+#ifdef GW_AB_NO_OBS_GSTORE
+    asm volatile("" :: "v"(v), "v"(voff));
+    (void)rs; (void)ioff;
+#else
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)voff + ioff, 0, 0);
+#endif
+}
+
 __device__ __forceinline__ double rld(double v, int l)
 {
     uint64_t b = __double_as_longlong(v);
@@ -720,86 +747,79 @@ __device__ __forceinline__ void table_remove(const Params& p, Smem& sm, const La
 }
 
 // ------------------------------------------------------------ observation
-// Observation stage geometry: int8 [A][S][SP], each window row padded to
-// SP = 4*ceil(S/4) bytes so a decoded table dword is written to LDS as is.
+// Observation stage: A*SS compact bytes (the env's outputs in order), then
+// the crowded-cell pair list; sized as int8 [A][S][SP], SP = 4*ceil(S/4)
+// (a window row as whole table dwords).
 __host__ __device__ constexpr int stage_pitch(int S) { return (S + 3) & ~3; }
 
-// Lane l's row-padded stage rows [S][SP] -> SS consecutive bytes at byte
-// l*SS of the stage (in place; lanes >= A untouched).  Byte i of the row
-// stream is window row i / S, column i % S.
+// Lane l's window rows, row-padded [S][NW] dwords in registers, -> SS
+// consecutive bytes at byte l*SS of the stage (the compact layout the store
+// reads: output m of the env is stage byte m).  Byte i of the row stream is
+// window row i / S, column i % S.  Lanes share the dwords at their span's
+// ends, written byte by byte.
 template <int S>
-__device__ __forceinline__ void compact_stage(Smem& sm, int A)
+__device__ __forceinline__ void write_compact(Smem& sm, int l, const uint32_t* rw)
 {
     constexpr int NW = (S + 3) / 4;
-    constexpr int SSP = S * stage_pitch(S);
     constexpr int SS = S * S;
     constexpr int CW = (SS + 3) / 4;            // stream dwords
-    const int l = lane_id();
-    uint32_t rw[S * NW];
-    const uint32_t* st32 = (const uint32_t*)sm.stage;
+    uint32_t seg[CW];
 #pragma unroll
-    for (int k = 0; k < S * NW; k++) rw[k] = l < A ? st32[l * (SSP / 4) + k] : 0u;
-    wave_sync();
-    if (l < A) {
-        uint32_t seg[CW];
+    for (int g = 0; g < CW; g++) {
+        // stream bytes 4g..4g+3 from at most two row dwords (one perm), or
+        // assembled byte by byte when they span three
+        int src[4], sb[4];
 #pragma unroll
-        for (int g = 0; g < CW; g++) {
-            // stream bytes 4g..4g+3 from at most two row dwords (one perm), or
-            // assembled byte by byte when they span three
-            int src[4], sb[4];
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int i = 4 * g + b < SS ? 4 * g + b : SS - 1;
-                const int r = i / S, c = i % S;
-                src[b] = r * NW + (c >> 2);
-                sb[b] = c & 3;
-            }
-            const int s0 = src[0];
-            int s1 = s0;
-#pragma unroll
-            for (int b = 1; b < 4; b++) if (src[b] != s0) s1 = src[b];
-            bool two = true;
-#pragma unroll
-            for (int b = 0; b < 4; b++) two = two && (src[b] == s0 || src[b] == s1);
-            if (two) {
-                // v_perm_b32(hi, lo, sel): selector byte k picks byte k of lo
-                // (0-3) or of hi (4-7)
-                uint32_t sel = 0;
-#pragma unroll
-                for (int b = 0; b < 4; b++) sel |= (uint32_t)((src[b] == s0 ? 0 : 4) + sb[b]) << (8 * b);
-                seg[g] = __builtin_amdgcn_perm(rw[s1], rw[s0], sel);
-            } else {
-                uint32_t v = 0;
-#pragma unroll
-                for (int b = 0; b < 4; b++) v |= ((rw[src[b]] >> (8 * sb[b])) & 0xffu) << (8 * b);
-                seg[g] = v;
-            }
+        for (int b = 0; b < 4; b++) {
+            const int i = 4 * g + b < SS ? 4 * g + b : SS - 1;
+            const int r = i / S, c = i % S;
+            src[b] = r * NW + (c >> 2);
+            sb[b] = c & 3;
         }
-        // memory dword k of this lane's span holds stream bytes [4k - s, 4k - s + 4)
-        const int s = (l * SS) & 3;
-        uint32_t* dst = (uint32_t*)sm.stage + ((l * SS) >> 2);
+        const int s0 = src[0];
+        int s1 = s0;
 #pragma unroll
-        for (int k = 0; k <= CW; k++) {
-            const uint32_t lo_w = k == 0 ? 0u : seg[k - 1];
-            const uint32_t hi_w = k < CW ? seg[k] : 0u;
-            const uint32_t val = (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (32 - 8 * s));
-            if (k >= 1 && 4 * k + 4 <= SS) {            // full for every s
+        for (int b = 1; b < 4; b++) if (src[b] != s0) s1 = src[b];
+        bool two = true;
+#pragma unroll
+        for (int b = 0; b < 4; b++) two = two && (src[b] == s0 || src[b] == s1);
+        if (two) {
+            // v_perm_b32(hi, lo, sel): selector byte k picks byte k of lo
+            // (0-3) or of hi (4-7)
+            uint32_t sel = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) sel |= (uint32_t)((src[b] == s0 ? 0 : 4) + sb[b]) << (8 * b);
+            seg[g] = __builtin_amdgcn_perm(rw[s1], rw[s0], sel);
+        } else {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) v |= ((rw[src[b]] >> (8 * sb[b])) & 0xffu) << (8 * b);
+            seg[g] = v;
+        }
+    }
+    // memory dword k of this lane's span holds stream bytes [4k - s, 4k - s + 4)
+    const int s = (l * SS) & 3;
+    uint32_t* dst = (uint32_t*)sm.stage + ((l * SS) >> 2);
+#pragma unroll
+    for (int k = 0; k <= CW; k++) {
+        const uint32_t lo_w = k == 0 ? 0u : seg[k - 1];
+        const uint32_t hi_w = k < CW ? seg[k] : 0u;
+        const uint32_t val = (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (32 - 8 * s));
+        if (k >= 1 && 4 * k + 4 <= SS) {            // full for every s
+            dst[k] = val;
+        } else {
+            const int lo = k == 0 ? s : 0;
+            const int hi = s + SS - 4 * k < 4 ? s + SS - 4 * k : 4;
+            if (lo == 0 && hi == 4) {
                 dst[k] = val;
             } else {
-                const int lo = k == 0 ? s : 0;
-                const int hi = s + SS - 4 * k < 4 ? s + SS - 4 * k : 4;
-                if (lo == 0 && hi == 4) {
-                    dst[k] = val;
-                } else {
-                    uint8_t* d8 = (uint8_t*)(dst + k);
+                uint8_t* d8 = (uint8_t*)(dst + k);
 #pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        if (b >= lo && b < hi) d8[b] = (uint8_t)(val >> (8 * b));
-                }
+                for (int b = 0; b < 4; b++)
+                    if (b >= lo && b < hi) d8[b] = (uint8_t)(val >> (8 * b));
             }
         }
     }
-    wave_sync();
 }
 
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
@@ -815,8 +835,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     constexpr int R = S / 2;
     constexpr int NW = (S + 3) / 4;           // stage dwords per window row
     constexpr int ND = NW + 1;                // table dwords covering S bytes at any alignment
-    constexpr int SP = stage_pitch(S);
-    constexpr int SSP = S * SP;
+    constexpr int SSP = S * stage_pitch(S);
     const int l = lane_id();
     const int A = p.A;
     // (gw_component OBSERVE: the one lane OO, whatever its done state)
@@ -884,10 +903,10 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
     // observation values (0 empty, enc, 0xFF = -1 off-grid); 0x80 marks a
     // crowded cell, resolved below; hidden cells become 0xFE = -2.
     uint32_t nev = 0;                         // crowded visible cells of this observer
+    uint32_t rw[S * NW];                      // this lane's window rows, row-padded
     auto stage_rows = [&](auto masked, auto hetero) {
         constexpr bool MASKED = decltype(masked)::value;
         constexpr bool HETERO = decltype(hetero)::value;
-        uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
         const uint32_t* t32 = (const uint32_t*)sm.tbl;
         uint32_t rows[S][ND];
         const int o0 = HETERO ? tbl_idx(p, L.r - vw, L.c - vw) : tbl_idx(p, L.r - R, L.c - R);
@@ -932,7 +951,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                 const uint32_t vm = (S - 4 * d >= 4) ? 0x80808080u
                                         : (0x80808080u & ((1u << (8 * (S - 4 * d))) - 1u));
                 nev += (uint32_t)__popc(w & vm & ~(w << 1));
-                st32[wr * NW + d] = w;
+                rw[wr * NW + d] = w;
             }
         }
     };
@@ -949,12 +968,12 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                 stage_rows(F(), F());
             }
         } else {
-            uint32_t* st32 = (uint32_t*)(sm.stage + l * SSP);
             // -2 rows; a row the store skips holds the 0x80 sentinel instead
             const uint32_t fill = ((skip >> l) & 1ull) ? 0x80808080u : 0xFEFEFEFEu;
 #pragma unroll
-            for (int k = 0; k < S * NW; k++) st32[k] = fill;
+            for (int k = 0; k < S * NW; k++) rw[k] = fill;
         }
+        write_compact<S>(sm, l, rw);
     }
     wave_sync();
     STAMP(stamp_base);
@@ -977,19 +996,22 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         // the reset placement); the value is the j-th member by seq.
         uint16_t* pairs = (uint16_t*)(sm.stage + A * SSP);
         if (nev) {
+            // this lane's compact span: dword k holds stream bytes 4k - s ..
             int q = (int)(ev_scan - nev);
-            const uint32_t* st32 = (const uint32_t*)(sm.stage + l * SSP);
+            constexpr int CW = (SS + 3) / 4;
+            const int s = (l * SS) & 3;
+            const uint32_t* st32 = (const uint32_t*)sm.stage + ((l * SS) >> 2);
 #pragma unroll
-            for (int wr = 0; wr < S; wr++) {
-#pragma unroll
-                for (int d = 0; d < NW; d++) {
-                    const uint32_t w = st32[wr * NW + d];
-                    const uint32_t vm = (S - 4 * d >= 4) ? 0x80808080u
-                                        : (0x80808080u & ((1u << (8 * (S - 4 * d))) - 1u));
-                    for (uint32_t m = w & vm & ~(w << 1); m; m &= m - 1) {
-                        const int wc = d * 4 + (int)(__builtin_ctz(m) >> 3);
-                        pairs[CIDX(q++, p.pair_cap, 20)] = (uint16_t)((l << 8) | (wr << 4) | wc);
-                    }
+            for (int k = 0; k <= CW; k++) {
+                const uint32_t w = st32[k];
+                // bytes b with 0 <= 4k + b - s < SS
+                const int lo = s - 4 * k, hi = SS + s - 4 * k;
+                uint32_t vm = 0x80808080u;
+                if (lo > 0) vm &= 0xffffffffu << (8 * lo);
+                if (hi < 4) vm &= hi <= 0 ? 0u : ((1u << (8 * hi)) - 1u);
+                for (uint32_t m = w & vm & ~(w << 1); m; m &= m - 1) {
+                    const int i = 4 * k + (int)(__builtin_ctz(m) >> 3) - s;
+                    pairs[CIDX(q++, p.pair_cap, 20)] = (uint16_t)((l << 8) | i);
                 }
             }
         }
@@ -1010,7 +1032,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             const int q = c0 + l;
             const bool act = q < P;
             const int pv = act ? (int)pairs[q] : 0;
-            const int o = pv >> 8, pwr = (pv >> 4) & 15, pwc = pv & 15;
+            const int o = pv >> 8, pi = pv & 255, pwr = pi / S, pwc = pi - pwr * S;
             const int orr = __shfl(L.r, o), occ = __shfl(L.c, o);
             const uint32_t oseq = __shfl(L.seq, o);
             const bool o_in = __shfl((int)L.in_grid, o) != 0;
@@ -1059,7 +1081,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                     if (r2 == (int)j) val = enc;
                 }
             }
-            if (act) sm.stage[o * SSP + pwr * SP + pwc] = (int8_t)val;
+            if (act) sm.stage[o * SS + pi] = (int8_t)val;
             rng.pos += (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
             rng.base = -1;
         }
@@ -1076,8 +1098,7 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
         const int ov = HV ? rl(vw, o) : R;
         for (int k0 = 0; k0 < SS; k0 += WAVE) {
             const int k = k0 + l;
-            const int sidx = o * SSP + (k / S) * SP + k % S;
-            const bool crowd = k < SS && (uint8_t)sm.stage[sidx] == CELL_CROWD;
+            const bool crowd = k < SS && (uint8_t)sm.stage[o * SS + k] == CELL_CROWD;
             uint64_t bits = __ballot(crowd);
             while (bits) {
                 const int kk = k0 + (int)__builtin_ctzll(bits);
@@ -1097,46 +1118,46 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
                     if (rank == j) { sel = m; break; }
                 }
                 const int val = rl(L.enc, sel);
-                if (l == 0) sm.stage[o * SSP + (kk / S) * SP + kk % S] = (int8_t)val;
+                if (l == 0) sm.stage[o * SS + kk] = (int8_t)val;
             }
         }
     }
     wave_sync();
     STAMP(stamp_base + 1);
 
-    // stage (int8) -> obs (int32).  First every lane compacts its own
-    // row-padded [S][SP] stage rows into SS consecutive bytes at l*SS (in
-    // place: all rows are read before any is written), so that output m is
-    // stage byte m; then lane-contiguous int4 stores of 4 consecutive
-    // outputs from one aligned stage dword each.  Rows the store skips hold
-    // the 0x80 sentinel: a dword of four sentinels is not stored, a mixed one
-    // stores -2 for them (max(v, -2): valid bytes are >= -2).
-    compact_stage<S>(sm, A);
+    // stage (int8, compact: output m is stage byte m) -> obs (int32):
+    // lane-contiguous int4 stores of 4 consecutive outputs from one aligned
+    // stage dword each.  Rows the store skips hold the 0x80 sentinel: a
+    // dword of four sentinels is not stored, a mixed one stores -2 for them
+    // (max(v, -2): valid bytes are >= -2).
     const int total = A * SS;
     int32_t* out = obs + (size_t)e * total;
     const uint32_t* cs = (const uint32_t*)sm.stage;
     if ((total & 3) == 0) {
+        // raw buffer stores on the env's obs row: the range check drops the
+        // tail past A*SS (no per-store bound test) and a skipped dword is sent
+        // out of range instead of branched around; offsets are immediates
         constexpr int NIT = (GW_MAX_AGENTS * SS + 4 * WAVE - 1) / (4 * WAVE);
-        constexpr int B = NIT < 7 ? NIT : 7;                    // LDS reads in flight
-        for (int k0 = 0; k0 < NIT && k0 * 4 * WAVE < total; k0 += B) {
-            uint32_t w[B];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, total * 4, BUF_RSRC_W3);
+        const uint32_t base = (uint32_t)l * 16u;
+        auto put = [&](int k, uint32_t w) {
+            uint32_t voff = (skip && w == 0x80808080u) ? 0x80000000u : base;
+            asm volatile("" : "+v"(voff));      // keeps k * 1024 an immediate offset
+            buf_store_i8x4(rs, voff, k * 4 * WAVE * 4, w);
+        };
+        if (total > (NIT - 1) * 4 * WAVE) {
+            // every iteration has live bytes: batches of LDS reads in flight
+            constexpr int B = NIT < 7 ? NIT : 7;
 #pragma unroll
-            for (int k = 0; k < B; k++) {
-                const int m = ((k0 + k) * WAVE + l) * 4;
-                w[k] = cs[(m < total ? m : 0) >> 2];
-            }
+            for (int k0 = 0; k0 < NIT; k0 += B) {
+                uint32_t w[B];
 #pragma unroll
-            for (int k = 0; k < B; k++) {
-                const int m = ((k0 + k) * WAVE + l) * 4;
-                if (m < total && (!skip || w[k] != 0x80808080u)) {
-                    int4 v = make_int4((int8_t)(w[k] & 0xff), (int8_t)((w[k] >> 8) & 0xff),
-                                       (int8_t)((w[k] >> 16) & 0xff), (int8_t)(w[k] >> 24));
-                    if (skip) {
-                        v.x = max(v.x, -2); v.y = max(v.y, -2); v.z = max(v.z, -2); v.w = max(v.w, -2);
-                    }
-                    *(int4*)(out + m) = v;
-                }
+                for (int k = 0; k < B; k++) if (k0 + k < NIT) w[k] = cs[(k0 + k) * WAVE + l];
+#pragma unroll
+                for (int k = 0; k < B; k++) if (k0 + k < NIT) put(k0 + k, w[k]);
             }
+        } else {
+            for (int k = 0; k * 4 * WAVE < total; k++) put(k, cs[k * WAVE + l]);
         }
     } else {
         for (int m = l; m < total; m += WAVE) {
@@ -2412,7 +2433,9 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
 
                 // ---- observations of the live agents (all_step_manager.py:68-71)
                 STAMP(4);
+#ifndef GW_AB_NO_OBS
                 observe_all<S, PLAIN>(p, e, sm, rng, L, obs_t);
+#endif
                 STAMP(5);
 
                 // ---- rewards, dones (:72-79, smart.py:101-111)
