@@ -11,6 +11,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(PKG, 'csrc', 'gw_engine.hip')
 INCLUDE = os.path.join(os.path.dirname(PKG), 'include', 'gw_engine.h')
 LIB = os.path.join(PKG, '_build', 'libgw_engine.so')
+# A/B runs of another in-tree build (tools/ab_*.py); never set by the product path
+if os.environ.get('GW_ENGINE_LIB'):
+    LIB = os.path.abspath(os.environ['GW_ENGINE_LIB'])
 # diagnostic build with in-kernel s_memtime stamps (tools/stamps.py); never the default
 LIB_STAMPS = os.path.join(PKG, '_build', 'libgw_engine_stamps.so')
 # diagnostic build with bounds / one-lane checks that record instead of faulting
