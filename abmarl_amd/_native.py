@@ -59,6 +59,7 @@ SIGNATURES = {
     'gw_num_passive': (_i32, [_vp]),
     'gw_turn_reset': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_turn_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    'gw_turn_rollout': (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     'gw_sim_reset': (_i32, [_vp, _vp, _vp, _vp]),
     'gw_sim_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_observe': (_i32, [_vp, _i32, _vp, _vp]),

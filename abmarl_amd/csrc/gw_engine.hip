@@ -2072,9 +2072,6 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_PROGRESS_PRIO
 #define GW_PROGRESS_PRIO 1
 #endif
-#ifndef GW_PARK_REGS
-#define GW_PARK_REGS 0
-#endif
 #ifndef GW_PREFETCH_ACTIONS
 #define GW_PREFETCH_ACTIONS 1
 #endif
@@ -2153,12 +2150,8 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
             mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
         } else if (t > 0) {
-#if GW_PARK_REGS
-            const int a0 = pa0, a1 = pa1, a2 = pa2;
-#else
             const int32_t* na = sm.nact + 3 * l;
             const int a0 = na[0], a1 = na[1], a2 = na[2];
-#endif
             mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
         }
         const bool prefetch = GW_PREFETCH_ACTIONS && t + 1 < p.nsteps;
@@ -2168,11 +2161,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         }
         nact_ok = false;
         auto park = [&]() {
-#if GW_PARK_REGS
-            if (prefetch) nact_ok = true;
-#else
             if (prefetch) { int32_t* na = sm.nact + 3 * l; na[0] = pa0; na[1] = pa1; na[2] = pa2; nact_ok = true; }
-#endif
         };
         if (need_tmpl) { table_template(p, sm); lanes_in = false; need_tmpl = false; }
         // NEXT_STEP auto-reset: the episode ended in the previous step, so this
@@ -3833,6 +3822,23 @@ gw_status gw_turn_step(gw_handle g, const int32_t* actions, int32_t* obs, double
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.returned = returned; p.turn = turn; p.acting = acting; p.horizon = horizon; p.err = err_flags;
     p.mode = PAC_STEP_TURN;
+    p.nsteps = 1; p.ad_in = all_done;       // all_done is in/out
+    HIPCHK(launch_pac(g, p, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_turn_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
+                          uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint8_t* returned,
+                          int32_t* turn, uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream)
+{
+    if (!g || n_steps <= 0 || !actions || !obs || !reward || !done || !all_done || !returned || !turn)
+        return GW_E_INVALID;
+    if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
+    Params p = g->base;
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.returned = returned; p.turn = turn; p.acting = acting; p.horizon = horizon; p.err = err_flags;
+    p.mode = PAC_STEP_TURN;
+    p.nsteps = n_steps; p.ad_in = all_done_in; p.ad_out = all_done_in;
     HIPCHK(launch_pac(g, p, (hipStream_t)stream));
     return GW_OK;
 }
@@ -4010,37 +4016,12 @@ gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32
     Params p = g->base;
     p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
     p.persistent_obs = 0;                  // every step has its own obs slab
-    if (!g->pacman) {
-        // one launch: each env runs its n_steps back to back (step_kernel,
-        // lane_step_kernel, wg_step_kernel)
-        p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
-        p.nsteps = n_steps; p.ad_in = all_done_in; p.skip_done_obs = skip_done_obs != 0;
-        p.ad_out = all_done_in;            // each env's wave reads it first, writes it last
-        HIPCHK(do_step(g, p, st));
-        return GW_OK;
-    }
-    // the Pacman kernel: one launch per step, __all__ carried
-    // from slab t-1 to slab t (their all_done is in/out)
-    const size_t EA = (size_t)g->E * g->A;
-    int32_t orows, ocols;
-    gw_obs_shape(g, &orows, &ocols);
-    const size_t obs_stride = EA * (size_t)orows * ocols;
-    for (int t = 0; t < n_steps; t++) {
-        uint8_t* ad_t = all_done + (size_t)t * g->E;
-        const uint8_t* ad_prev = t == 0 ? all_done_in : all_done + (size_t)(t - 1) * g->E;
-        if (ad_prev) HIPCHK(hipMemcpyAsync(ad_t, ad_prev, (size_t)g->E, hipMemcpyDeviceToDevice, st));
-        else HIPCHK(hipMemsetAsync(ad_t, 0, (size_t)g->E, st));
-        p.actions = actions + (size_t)t * EA * p.act_dim;
-        p.obs = obs + (size_t)t * obs_stride;
-        p.reward = reward + (size_t)t * EA;
-        p.done = done + (size_t)t * EA;
-        p.all_done = ad_t;
-        p.nsteps = 1; p.ad_in = ad_t;
-        HIPCHK(do_step(g, p, st));
-    }
-    if (all_done_in)
-        HIPCHK(hipMemcpyAsync(all_done_in, all_done + (size_t)(n_steps - 1) * g->E, (size_t)g->E,
-                              hipMemcpyDeviceToDevice, st));
+    // one launch: each env runs its n_steps back to back (step_kernel,
+    // lane_step_kernel, wg_step_kernel, pac_kernel)
+    p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
+    p.nsteps = n_steps; p.ad_in = all_done_in; p.skip_done_obs = skip_done_obs != 0;
+    p.ad_out = all_done_in;                // each env's wave reads it first, writes it last
+    HIPCHK(do_step(g, p, st));
     return GW_OK;
 }
 

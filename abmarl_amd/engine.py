@@ -193,6 +193,63 @@ class GridWorldEngine:
                 _ptr(self.err), _stream()), 'gw_turn_step')
         return self.obs, self.reward, self.done, self.all_done, ret, turn
 
+    def turn_rollout_buffers(self, n_steps):
+        """Per-turn output slabs for turn_rollout(): rollout_buffers plus
+        returned[n][E][A] and turn[n][E]."""
+        out = self.rollout_buffers(n_steps)
+        out['returned'] = torch.empty((n_steps, self.E, self.A), dtype=torch.uint8, device=self.device)
+        out['turn'] = torch.empty((n_steps, self.E), dtype=torch.int32, device=self.device)
+        return out
+
+    def turn_rollout(self, actions, horizon=0, out=None):
+        """K = actions.shape[0] consecutive turn_step calls in ONE launch
+        (gw_turn_rollout): turn t's outputs in slab t of `out`
+        (turn_rollout_buffers).  The '__all__' before turn 0 is self.all_done
+        (the previous call's); afterwards it holds the last turn's.  obs rows
+        of lanes not returned in a turn are left unwritten (mask: returned)."""
+        K = int(actions.shape[0])
+        assert actions.dtype == torch.int32 and actions.is_contiguous()
+        assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
+        assert actions.device == self.device, (actions.device, self.device)
+        out = self.turn_rollout_buffers(K) if out is None else out
+        self._check_rollout_buffers(K, out)
+        for k, shape, dt in (('returned', (self.E, self.A), torch.uint8), ('turn', (self.E,), torch.int32)):
+            t = out[k]
+            assert t.dtype == dt and t.is_contiguous() and t.device == self.device, k
+            assert tuple(t.shape[1:]) == shape and t.shape[0] >= K, (k, tuple(t.shape))
+        self._turn_bufs()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_turn_rollout(
+                self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                _ptr(out['all_done']), _ptr(self.all_done), _ptr(out['returned']), _ptr(out['turn']),
+                _ptr(self.acting), int(horizon), _ptr(self.err), _stream()), 'gw_turn_rollout')
+        # the single-call buffers follow the last turn
+        self.turn.copy_(out['turn'][K - 1])
+        self._check_debug('gw_turn_rollout')
+        return out
+
+    def turn_rollout_launcher(self, actions, horizon=0, out=None):
+        """A prepared gw_turn_rollout launch (see rollout_launcher); the
+        single-call turn buffer is not refreshed by it."""
+        K = int(actions.shape[0])
+        assert actions.dtype == torch.int32 and actions.is_contiguous()
+        assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
+        assert torch.cuda.current_device() == self.device.index, "launcher: the engine's device must be current"
+        out = self.turn_rollout_buffers(K) if out is None else out
+        self._check_rollout_buffers(K, out)
+        fn = self.L.gw_turn_rollout
+        args = (self.h, K, _ptr(actions), _ptr(out['obs']), _ptr(out['reward']), _ptr(out['done']),
+                _ptr(out['all_done']), _ptr(self.all_done), _ptr(out['returned']), _ptr(out['turn']),
+                _ptr(self.acting), int(horizon), _ptr(self.err), _stream())
+        keep = (actions, out)
+
+        def launch():
+            st = fn(*args)
+            if st != 0:
+                _native.check(st, 'gw_turn_rollout')
+            return keep[1]
+        return launch
+
     def sim_reset(self, mask=None):
         """SmartGWS.reset only (no observation drawn)."""
         with torch.cuda.device(self.device):

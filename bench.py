@@ -79,6 +79,17 @@ def pacman_turn_bytes(E, A, HW, pwords):
     return E * (A * (8 + 8 + 1 + 1 + 2 * 29) + 4 * HW + 8 * pwords + 1 + 4 + 8 + 8 + 16 + 16)
 
 
+def pacman_turn_rollout_bytes(E, A, HW, pwords, n_steps, returned):
+    """Algorithmic HBM bytes of one gw_turn_rollout launch of n_steps turns:
+    per turn and lane actions read 8 (move + present), reward 8 + done 1 +
+    returned 1; per turn and env all_done 1 + turn 4; 4*HW per returned obs
+    row (`returned` over the launch, approximated by the acting agent-steps:
+    one row per turn except at an episode's end); per launch the state
+    read+write of pacman_turn_bytes."""
+    return (n_steps * E * (A * (8 + 8 + 1 + 1) + 1 + 4) + 4 * HW * returned +
+            E * (A * 2 * 29 + 8 * pwords + 8 + 8 + 16 + 16))
+
+
 def step_bytes(E, A, S):
     """Algorithmic HBM bytes of one step launch:
     per entity slot: actions 12 + obs 4*S*S + reward 8 + done 1 +
@@ -219,7 +230,35 @@ def quick_config(name, steps=200, warmup=400):
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     acting = int(eng.acting.sum().item()) - a0
     roll = None
-    if name != 'pacman':
+    if name == 'pacman':
+        # the same engine as gw_turn_rollout fragments of 50 turns on actions
+        # resident in HBM
+        F = 50
+        acts = torch.empty((steps,) + tuple(eng.actions.shape), dtype=torch.int32, device=eng.device)
+        for t in range(steps):
+            eng.random_actions(key, warmup + steps + t, out=acts[t])
+        out = eng.turn_rollout_buffers(F)
+        eng.turn_rollout(acts[:F], horizon=horizon, out=out)           # untimed first launch
+        revs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(F, steps, F)]
+        torch.cuda.synchronize()
+        r0 = int(eng.acting.sum().item())
+        t1 = time.perf_counter()
+        for i, ev in zip(range(F, steps, F), revs):
+            ev[0].record()
+            eng.turn_rollout(acts[i:i + F], horizon=horizon, out=out)
+            ev[1].record()
+        torch.cuda.synchronize()
+        rdt = time.perf_counter() - t1
+        ra = int(eng.acting.sum().item()) - r0
+        lms = float(np.mean([a.elapsed_time(b) for a, b in revs]))
+        rb = pacman_turn_rollout_bytes(E, eng.A, cc.rows * cc.cols, (eng.n_passive + 31) // 32, F,
+                                       ra / len(revs))
+        roll = {'value': round(ra / rdt, 1), 'ms_per_step': round(rdt / (steps - F) * 1e3, 4),
+                'launch_ms': round(lms, 4), 'steps_per_launch': F, 'bytes_per_launch': round(rb),
+                'achieved_GBs': round(rb / (lms * 1e-3) / 1e9, 2),
+                'protocol': 'gw_turn_rollout fragments (one launch per 50 turns) on actions resident in HBM'}
+    else:
         # the same engine as gw_rollout fragments of 100 steps on actions
         # resident in HBM (the headline line's protocol)
         F = 100
@@ -425,7 +464,7 @@ def main():
         acts_all = torch.empty((nfrag + args.steps,) + tuple(eng.actions.shape),
                                dtype=torch.int32, device=eng.device)
         acts = acts_all[:nfrag]
-        out = eng.rollout_buffers(nfrag)
+        out = (eng.turn_rollout_buffers if turn else eng.rollout_buffers)(nfrag)
         # untimed pre-roll + warmup as fragments of up to nfrag steps, the
         # last one exactly F steps: it writes the same output slabs and reads
         # actions laid out as the timed fragments'
@@ -450,15 +489,19 @@ def main():
                 # the timed steps' actions (inputs resident in HBM before timing)
                 for s in range(args.steps):
                     eng.random_actions(key, untimed + s, env_offset=first, out=all_acts[s])
-            eng.rollout(acts[:f], horizon=args.horizon, autoreset=mode, skip_done_obs=True, out=out)
+            if turn:
+                eng.turn_rollout(acts[:f], horizon=args.horizon, out=out)
+            else:
+                eng.rollout(acts[:f], horizon=args.horizon, autoreset=mode, skip_done_obs=True, out=out)
             t += f
             if k == len(sizes) - 2:
                 torch.cuda.synchronize()
                 eng.check_errors(allow=allow)
         # prepared launches (validated here, one ctypes call each when timed)
         # and their events, created by a first record outside the timed region
-        launches = [eng.rollout_launcher(all_acts[i:i + f], horizon=args.horizon, autoreset=mode,
-                                         skip_done_obs=True, out=out) for i, f in frags]
+        launches = [eng.turn_rollout_launcher(all_acts[i:i + f], horizon=args.horizon, out=out) if turn
+                    else eng.rollout_launcher(all_acts[i:i + f], horizon=args.horizon, autoreset=mode,
+                                              skip_done_obs=True, out=out) for i, f in frags]
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in frags]
         for a_, b_ in evs:
@@ -494,7 +537,7 @@ def main():
                     acting_local=acting)
 
     mode = 'next_step' if turn else args.autoreset
-    rollout = args.mode == 'rollout' and not turn
+    rollout = args.mode == 'rollout'
     other = 'same_step' if mode == 'next_step' else 'next_step'
     eng, r = run(mode, rollout)
     A, n_passive = eng.A, eng.n_passive
@@ -510,7 +553,10 @@ def main():
         value = acting_all / dt_all
         S = cc.obs_side
         F = r['steps_per_launch']
-        if rollout:
+        if rollout and turn:
+            nbytes = pacman_turn_rollout_bytes(E_local, A, cc.rows * cc.cols, (n_passive + 31) // 32, F,
+                                               r['acting_local'] * F / args.steps)
+        elif rollout:
             # per launch: the local rank's acting agent-steps scaled to one launch
             nbytes = rollout_bytes(E_local, A, S, F, r['acting_local'] * F / args.steps, cc.act_dim)
         elif args.workload == 'team_battle' or args.workload == 'maze':
@@ -522,7 +568,8 @@ def main():
         scaling = 'strong' if strong else 'weak'
         workload = (f'{wdesc}, {E_local} envs per GPU ({int(envs_all)} in total, {scaling} scaling), '
                     f'horizon {args.horizon}, {mode} auto-reset, {args.preroll}-step pre-roll, ' +
-                    (f'gw_rollout fragments of {F} steps on actions resident in HBM (one launch '
+                    (f'{"gw_turn_rollout" if turn else "gw_rollout"} fragments of {F} steps on actions '
+                     f'resident in HBM (one launch '
                      f'per fragment, obs written for the agents that get one)' if rollout else
                      'one step launch per step + the Philox action kernel'))
         if args.workload != 'team_battle':

@@ -419,10 +419,10 @@ gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* arg
    skip_done_obs = 1: obs rows of entities that get no observation in a
    step (done before it, or not grid observers) are left unwritten in that
    step's slab instead of being filled with -2 (the reference returns no obs
-   for them; mask with done).  The Pacman kernel runs the fragment as n_steps
-   launches (same results, rows always written); the workgroup-per-env
-   kernel runs it in one launch with the env's state passing through HBM
-   between its steps (rows always written).
+   for them; mask with done).  The Pacman kernel runs it in one launch too
+   (rows always written); the workgroup-per-env kernel runs it in one
+   launch with the env's state passing through HBM between its steps (rows
+   always written).
    The handle's persistent obs rows (gw_config.persistent_obs) are not used. */
 gw_status gw_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
                      uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint64_t* acting,
@@ -465,6 +465,20 @@ gw_status gw_turn_reset(gw_handle h, const uint8_t* mask, int32_t* obs, uint8_t*
 gw_status gw_turn_step(gw_handle h, const int32_t* actions, int32_t* obs, double* reward,
                        uint8_t* done, uint8_t* all_done, uint8_t* returned, int32_t* turn,
                        uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream);
+
+/* n_steps consecutive gw_turn_step calls in ONE launch (each env's wave runs
+   its turns back to back; lanes, cell table, food bits and stream stay on
+   chip): actions[t] feeds turn t, whose outputs go to slab t of
+     obs device int32[n][E][A][rows][cols] (rows of lanes not returned in
+         turn t are left unwritten: mask with returned),
+     reward double[n][E][A], done / returned uint8[n][E][A],
+     all_done uint8[n][E], turn int32[n][E];
+   all_done_in device uint8[E] or NULL: in/out as in gw_rollout (the
+   '__all__' before turn 0; overwritten with the last turn's).            */
+gw_status gw_turn_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32_t* obs,
+                          double* reward, uint8_t* done, uint8_t* all_done, uint8_t* all_done_in,
+                          uint8_t* returned, int32_t* turn, uint64_t* acting, int32_t horizon,
+                          uint32_t* err_flags, void* stream);
 
 /* The simulation alone, for a manager that lives in the host (the dict API):
    gw_sim_reset = SmartGWS.reset (no observation drawn); gw_sim_step =

@@ -281,3 +281,91 @@ def test_allstep_autoreset_vs_oracle(oracle_mod, mode):
     torch.cuda.synchronize()
     mt = eng.get_state()['mt'].cpu().numpy().view(np.uint32)
     assert (mt[:, :625] == orc.state()['mt'][:, :625]).all(), "RNG state"
+
+
+def _pac_pair(E, run, stagger=0):
+    import torch
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    cc = _sim().compiled()
+    engs = [GridWorldEngine(cc, E, seeds=env_seeds(E, run=run)) for _ in range(2)]
+    for eng in engs:
+        eng.turn_reset()
+        eng.all_done.zero_()
+        if stagger:
+            eng.set_state(steps=torch.as_tensor((np.arange(E) * stagger // E).astype(np.int32),
+                                                device=eng.device))
+    return engs
+
+
+def _same_state(a, b):
+    sa, sb = a.get_state(), b.get_state()
+    for k in ('pos', 'health', 'flags', 'seq', 'steps'):
+        assert (sa[k].cpu().numpy() == sb[k].cpu().numpy()).all(), k
+    assert (sa['mt'].cpu().numpy()[:, :625] == sb['mt'].cpu().numpy()[:, :625]).all(), 'RNG'
+    xa, xb = a.get_aux_state(), b.get_aux_state()
+    for k in xa:
+        assert (xa[k].cpu().numpy() == xb[k].cpu().numpy()).all(), k
+    assert (a.acting.cpu().numpy() == b.acting.cpu().numpy()).all(), 'acting'
+    assert (a.err.cpu().numpy() == b.err.cpu().numpy()).all(), 'err'
+
+
+@pytest.mark.parametrize('E,frags,horizon', [(2048, (1, 17, 40, 100), 60), (16384, (50, 50), 200)])
+def test_turn_rollout_matches_turn_steps(E, frags, horizon):
+    """gw_turn_rollout (K turns in one launch) against K gw_turn_step calls on
+    an engine with the same seeds, bit for bit: every turn's returned rows
+    of obs, reward bits, done, returned, turn, __all__, then the engine
+    state.  (gw_turn_step itself is pinned to the oracle above.)  16384
+    envs with 50-turn fragments is the bench's config-5 launch shape."""
+    import torch
+    a, b = _pac_pair(E, run=11, stagger=horizon)
+    t = 0
+    for f in frags:
+        acts = torch.empty((f,) + tuple(a.actions.shape), dtype=torch.int32, device=a.device)
+        for s in range(f):
+            a.random_actions(41, t + s, out=acts[s])
+        out = a.turn_rollout(acts, horizon=horizon)
+        for s in range(f):
+            obs, r, d, ad, ret, turn = b.turn_step(acts[s].contiguous(), horizon=horizon)
+            rt = ret.cpu().numpy()
+            assert (out['returned'][s].cpu().numpy() == rt).all(), f"turn {t + s}: returned"
+            assert (out['turn'][s].cpu().numpy() == turn.cpu().numpy()).all(), f"turn {t + s}: turn"
+            assert (out['all_done'][s].cpu().numpy() == ad.cpu().numpy()).all(), f"turn {t + s}: __all__"
+            assert (out['reward'][s].cpu().numpy().view(np.uint64) ==
+                    r.cpu().numpy().view(np.uint64)).all(), f"turn {t + s}: reward"
+            assert (out['done'][s].cpu().numpy() == d.cpu().numpy()).all(), f"turn {t + s}: done"
+            rb = rt.astype(bool)
+            assert (out['obs'][s].cpu().numpy()[rb] == obs.cpu().numpy()[rb]).all(), f"turn {t + s}: obs"
+        t += f
+    assert (a.all_done.cpu().numpy() == b.all_done.cpu().numpy()).all()
+    assert (a.turn.cpu().numpy() == b.turn.cpu().numpy()).all()
+    _same_state(a, b)
+
+
+@pytest.mark.parametrize('mode', ['next_step', 'same_step'])
+def test_allstep_rollout_matches_steps(mode):
+    """gw_rollout on the Pacman program (one launch per fragment) against
+    single AllStepManager steps with auto-reset, bit for bit."""
+    import torch
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    cc = _sim().compiled()
+    E, horizon = 1024, 45
+    a, b = [GridWorldEngine(cc, E, seeds=env_seeds(E, run=12)) for _ in range(2)]
+    for eng in (a, b):
+        eng.reset()
+        eng.all_done.zero_()
+    step_b = b.step_autoreset_next if mode == 'next_step' else b.step_autoreset
+    t = 0
+    for f in (1, 9, 64):
+        acts = torch.empty((f,) + tuple(a.actions.shape), dtype=torch.int32, device=a.device)
+        for s in range(f):
+            a.random_actions(43, t + s, out=acts[s])
+        out = a.rollout(acts, horizon=horizon, autoreset=mode)
+        for s in range(f):
+            obs, r, d, ad = step_b(acts[s].contiguous(), horizon=horizon)
+            assert (out['all_done'][s].cpu().numpy() == ad.cpu().numpy()).all(), f"step {t + s}: __all__"
+            assert (out['reward'][s].cpu().numpy().view(np.uint64) ==
+                    r.cpu().numpy().view(np.uint64)).all(), f"step {t + s}: reward"
+            assert (out['done'][s].cpu().numpy() == d.cpu().numpy()).all(), f"step {t + s}: done"
+            assert (out['obs'][s].cpu().numpy() == obs.cpu().numpy()).all(), f"step {t + s}: obs"
+        t += f
+    _same_state(a, b)
