@@ -235,6 +235,13 @@ __device__ __forceinline__ bool rlb(bool v, int l) { return __builtin_amdgcn_rea
 
 // raw buffer resource word 3 for gfx9 (data format 32, no swizzle, no stride)
 #define BUF_RSRC_W3 0x00020000
+// an offset past any buffer's range (< 2^31 bytes): the store is dropped
+#define BUF_OOB ((int)0x80000000)
+// cache policy of the observation stores: slc (streaming, non-temporal),
+// measured -11..16% on the headline workload
+#ifndef GW_OBS_STORE_AUX
+#define GW_OBS_STORE_AUX 2
+#endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // four observation bytes (valid values >= -2, 0x80 = skipped) -> four int32
 // max(sext(byte), -2) with SDWA byte selects (one VALU per output), stored
@@ -256,9 +263,6 @@ __device__ __forceinline__ void buf_store_i8x4(__amdgpu_buffer_rsrc_t rs, uint32
     asm volatile("" :: "v"(v), "v"(voff));
     (void)rs; (void)ioff;
 #else
-#ifndef GW_OBS_STORE_AUX
-#define GW_OBS_STORE_AUX 2      // slc: streaming (non-temporal) stores, measured -11..16% on the headline
-#endif
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)voff + ioff, 0, GW_OBS_STORE_AUX);
 #endif
 }
@@ -3570,6 +3574,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
                        (p.static_bits ? 4 * (size_t)((HW + 31) / 32) : 0);
         const size_t static_lds = 4 * GW_MT_N;
         if (g->smem_lane + static_lds > 64 * 1024) able = false;
+        // its per-step slabs are addressed by 32-bit buffer offsets
+        if ((size_t)n_envs * A * S * S * 4 >= ((size_t)1 << 31)) able = false;
         if (cfg->env_per_lane > 0 && !able) {
             set_err("env_per_lane: the one-lane-per-env kernel runs MazeNavigation with the navigator and "
                     "the target at initial positions as its only dynamic entities");
