@@ -10,8 +10,10 @@ GW_MAX_LANES = 256
 GW_KERNEL_WAVE, GW_KERNEL_WORKGROUP, GW_KERNEL_PACMAN, GW_KERNEL_LANE = 0, 1, 2, 3
 GW_MAX_ENTITIES = 4096
 GW_MAX_ENC = 15
-GW_MAX_CELLS = 4096
-GW_MAX_RANGE = 7
+GW_MAX_CELLS = 16384
+GW_MAX_RANGE = 64
+GW_MAX_ATTACK_RANGE = 7
+GW_FIXED_RANGE = 7          # windows up to this range are compiled per side (engine-internal)
 GW_ACT_DIM = 3
 GW_MT_N = 624
 GW_MT_STRIDE = 704

@@ -70,7 +70,7 @@ SIGNATURES = {
 }
 
 
-PART_SIDES = (1, 3, 5, 7, 9, 11, 13, 15)   # observation window sides S = 2*range+1
+PART_SIDES = (1, 3, 5, 7, 9, 11, 13, 15, 0)   # observation window sides S = 2*range+1; 0: any S > 15
 
 
 def build(force=False, verbose=False, stamps=False, checks=False, out=None, extra_flags=()):

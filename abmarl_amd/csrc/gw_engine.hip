@@ -58,6 +58,9 @@
 #define MT_CACHE 640        // [64] tempered key[cbase + i]
 #define SEQ_RENORM (1u << 23)
 #define CELL_CROWD 0x80u
+// observation windows up to this range (S <= 15) are compiled per window side
+// (the parts, -DGW_PART_S); wider ones run the generic path (part 0)
+#define GW_FIXED_RANGE 7
 #define CELL_OFF 0xFFu
 // lane_step_kernel (gw_lane.inc): lanes per env for an S x S window (the
 // window's cell count rounded up to 16, 32 or 64; host and device)
@@ -149,8 +152,8 @@ struct Params {
     // hidden cells due to static blockers for an entity at `cell`, range r:
     // smask_off[r] + cell * mask_words(r) (smask_off[r] < 0: not built)
     const uint32_t* smask;
-    int32_t shadow_off[GW_MAX_RANGE + 1];
-    int32_t smask_off[GW_MAX_RANGE + 1];
+    int32_t shadow_off[GW_FIXED_RANGE + 1];
+    int32_t smask_off[GW_FIXED_RANGE + 1];
     // Pacman program (GW_SIM_PACMAN, gw_pacman.inc)
     int32_t obs_kind, pacman, mode, obs_lane;
     int32_t tunnel[4];
@@ -195,8 +198,12 @@ struct Params {
     int32_t hetero_view;
     const uint32_t* hshadow;
     const uint32_t* hsmask;
-    int32_t hshadow_off[GW_MAX_RANGE + 1];
-    int32_t hsmask_off[GW_MAX_RANGE + 1];
+    int32_t hshadow_off[GW_FIXED_RANGE + 1];
+    int32_t hsmask_off[GW_FIXED_RANGE + 1];
+    // the generic window path (observe_big, obs_side > 2 * GW_FIXED_RANGE + 1)
+    int32_t obs_side;                      // S at run time
+    const int32_t* sblk;                   // static blocking entities: (row << 16) | col
+    int32_t n_sblk;
 };
 
 __host__ __device__ inline int mask_words(int r)
@@ -831,8 +838,8 @@ __device__ __forceinline__ void write_compact(Smem& sm, int l, const uint32_t* r
 
 // PositionCenteredEncodingObserver.get_obs for every live lane; S = 2R+1.
 template <int S, bool PLAIN = false>
-__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
-                                            int32_t* obs, int stamp_base = 8)
+__device__ __forceinline__ void observe_fixed(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
+                                              int32_t* obs, int stamp_base = 8)
 {
     // PLAIN (step_kernel<S, 1>): no blocking entities, one view range, every observer
     const bool HV = !PLAIN && p.hetero_view, BL = !PLAIN && p.blockers, LB = !PLAIN && p.lane_blockers;
@@ -1172,6 +1179,109 @@ __device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rn
             if (!((skip >> (m / SS)) & 1ull)) out[m] = v < -2 ? -2 : v;
         }
     }
+}
+
+// PositionCenteredEncodingObserver.get_obs (observer.py:204-250) for windows
+// wider than the compiled parts (S = p.obs_side > 2 * GW_FIXED_RANGE + 1, a
+// view range up to the grid's size and beyond): one observer at a time, in
+// lane (= agents dict) order, the wave covering its S x S slot 64 cells at a
+// time in row-major order, each cell's value computed straight from the cell
+// table and stored (no stage): -1 off the grid, -2 outside the observer's own
+// range (hetero view: its window sits top-left in the slot) and behind
+// blocking entities (create_grid_and_mask, utils.py:46-115, via
+// shadow_hides for every blocking lane and static blocker in range), 0 for
+// the observer's own cell when it is alone there and observe_self is off,
+// and for a crowded cell np.random.choice over the occupants' encodings in
+// insertion (seq) order without the observer when observe_self is off --
+// the draws in (observer, row, col) order as in the reference's loops.
+__device__ __noinline__ void observe_big(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, int32_t* obs)
+{
+    const int S = p.obs_side, R = S / 2, SS = S * S;
+    const int l = lane_id(), A = p.A;
+    const int OO = p.obs_only;
+    const bool obs_me = (OO >= 0 ? l == OO : (l < A && L.live)) && (L.kind & GW_K_GRID_OBSERVER);
+    const uint64_t skip = p.persistent_obs ? __ballot(l < A && L.obs_m2 && !obs_me)
+                        : (p.skip_done_obs ? __ballot(l < A && !obs_me) : 0ull);
+    if (l < A) L.obs_m2 = p.persistent_obs && !obs_me;
+    const uint64_t observers = __ballot(obs_me);
+    const uint64_t blk = p.lane_blockers ? __ballot(l < A && L.active && (L.kind & GW_K_BLOCKING)) : 0ull;
+    for (int o = 0; o < A; o++) {
+        int32_t* out = obs + ((size_t)e * A + o) * SS;
+        if (!((observers >> o) & 1ull)) {
+            if (!((skip >> o) & 1ull))
+                for (int k = l; k < SS; k += WAVE) __builtin_nontemporal_store(-2, out + k);
+            continue;
+        }
+        const int orr = rl(L.r, o), oc = rl(L.c, o);
+        const bool o_in = rlb(L.in_grid, o);
+        const int vw = p.hetero_view ? rl(L.view, o) : R;
+        const int D = 2 * vw + 1;
+        const int ocell = orr * p.W + oc;
+        for (int k0 = 0; k0 < SS; k0 += WAVE) {
+            const int k = k0 + l;
+            const int wr = k / S, wc = k - wr * S;
+            const bool inwin = k < SS && wr < D && wc < D;
+            const int dr = wr - vw, dc = wc - vw;             // the cell's offset from the observer
+            const int gr = orr + dr, gc = oc + dc;
+            // create_grid_and_mask: a hidden cell is -2 on or off the grid.
+            // (the blockers' readlanes run under the full wave: a readlane
+            // inside the divergent branch could read a lane the branch left
+            // inactive)
+            bool hid = false;
+            for (uint64_t it = blk; it; it &= it - 1) {
+                const int b = first_lane(it);
+                const int br = rl(L.r, b) - orr, bc = rl(L.c, b) - oc;
+                if (br >= -vw && br <= vw && bc >= -vw && bc <= vw && (br != 0 || bc != 0))
+                    hid = hid || (inwin && shadow_hides(br, bc, dr, dc));
+            }
+            for (int q = 0; q < p.n_sblk; q++) {
+                const int32_t sc = p.sblk[q];
+                const int br = (sc >> 16) - orr, bc = (sc & 0xffff) - oc;
+                if (br >= -vw && br <= vw && bc >= -vw && bc <= vw && (br != 0 || bc != 0))
+                    hid = hid || (inwin && shadow_hides(br, bc, dr, dc));
+            }
+            int val = -2;
+            bool crowd = false;
+            if (inwin && !hid) {
+                if (gr < 0 || gr >= p.H || gc < 0 || gc >= p.W) {
+                    val = -1;
+                } else {
+                    const uint32_t b = sm.tbl[tbl_idx(p, gr, gc)];
+                    if (b == CELL_CROWD) crowd = true;
+                    else if (!p.observe_self && o_in && gr * p.W + gc == ocell) val = 0;
+                    else val = (int)(int8_t)b;
+                }
+            }
+            for (uint64_t it = __ballot(crowd); it; it &= it - 1) {
+                const int kl = first_lane(it);
+                const int cr = rl(gr, kl), cc = rl(gc, kl);
+                const bool mem = l < A && L.in_grid && L.r == cr && L.c == cc && (p.observe_self || l != o);
+                const uint64_t mm = __ballot(mem);
+                const int n = __popcll(mm);
+                CHECK(n >= 1, 11, cr * 1000 + cc, o);
+                const uint32_t j = rng.interval((uint32_t)(n - 1));
+                // the j-th member in insertion (seq) order
+                int sel = first_lane(mm);
+                for (uint64_t jt = mm; jt; jt &= jt - 1) {
+                    const int m = first_lane(jt);
+                    const uint32_t sq = rl(L.seq, m);
+                    const uint32_t rank = (uint32_t)__popcll(__ballot(mem && L.seq < sq));
+                    if (rank == j) { sel = m; break; }
+                }
+                const int v = rl(L.enc, sel);
+                if (l == kl) val = v;
+            }
+            if (k < SS) __builtin_nontemporal_store(val, out + k);
+        }
+    }
+}
+
+template <int S, bool PLAIN = false>
+__device__ __forceinline__ void observe_all(const Params& p, int e, Smem& sm, Rng& rng, Lane& L,
+                                            int32_t* obs, int stamp_base = 8)
+{
+    if constexpr (S == 0) observe_big(p, e, sm, rng, L, obs);
+    else observe_fixed<S, PLAIN>(p, e, sm, rng, L, obs, stamp_base);
 }
 
 // ------------------------------------------------------------ attack
@@ -2022,7 +2132,7 @@ template <int S, bool PLAIN = false>
 __device__ __forceinline__ void reset_env(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, uint32_t& ctr,
                                           bool fused, int32_t* obs)
 {
-    constexpr int SS = S * S;
+    const int SS = S ? S * S : p.obs_side * p.obs_side;
     uint32_t err = 0;
     // fused: the LDS table holds the end-of-step grid; empty the lanes' cells
     // (static entities stay) instead of re-reading the template
@@ -2097,7 +2207,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
-    constexpr int SS = S * S;
+    const int SS = S ? S * S : p.obs_side * p.obs_side;
     STAMP(0);
     STAMP_WAVE(60, true);
     Smem sm = carve(smem_raw, p);
@@ -2912,12 +3022,23 @@ typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
     hipError_t GW_PART_CAT(gw_part_attr_, S_)(int, size_t);
 GW_PART_DECL(1) GW_PART_DECL(3) GW_PART_DECL(5) GW_PART_DECL(7)
 GW_PART_DECL(9) GW_PART_DECL(11) GW_PART_DECL(13) GW_PART_DECL(15)
+GW_PART_DECL(0)   // the generic window path: S at run time (> 2 * GW_FIXED_RANGE + 1)
 
 #ifdef GW_PART_S
 hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsigned block, size_t smem,
                                                    hipStream_t st, const void* params)
 {
     const Params& p = *static_cast<const Params*>(params);
+#if GW_PART_S == 0
+    // the generic window path: the one-wave step / reset / component kernels
+    switch (kind) {
+    case PK_STEP: hipLaunchKernelGGL((step_kernel<0, 0>), dim3(grid), dim3(block), smem, st, p); break;
+    case PK_RESET: hipLaunchKernelGGL(reset_kernel<0>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_COMP: hipLaunchKernelGGL(comp_kernel<0>, dim3(grid), dim3(block), smem, st, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+#else
     constexpr int S = GW_PART_S;
     switch (kind) {
     case PK_STEP: hipLaunchKernelGGL((step_kernel<S, 0>), dim3(grid), dim3(block), smem, st, p); break;
@@ -2931,10 +3052,18 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+#endif
 }
 
 hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
 {
+#if GW_PART_S == 0
+    const void* k0 = kind == PK_STEP ? (const void*)step_kernel<0, 0>
+                   : kind == PK_RESET ? (const void*)reset_kernel<0>
+                   : kind == PK_COMP ? (const void*)comp_kernel<0> : nullptr;
+    if (!k0) return hipErrorInvalidValue;
+    return hipFuncSetAttribute(k0, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+#else
     constexpr int S = GW_PART_S;
     const void* k = kind == PK_STEP ? (const void*)step_kernel<S, 0>
                   : kind == PK_STEP_TB ? (const void*)step_kernel<S, 1>
@@ -2945,6 +3074,7 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
                   : kind == PK_WG_COMP ? (const void*)wg_comp_kernel<S>
                                        : (const void*)wg_reset_kernel<S>;
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+#endif
 }
 #else   // ------------------------------------------------------- host part
 
@@ -2961,6 +3091,7 @@ struct gw_engine {
     uint32_t* d_smask;
     uint32_t* d_hshadow;       // slot-geometry LUTs (observers with different ranges)
     uint32_t* d_hsmask;
+    int32_t* d_sblk;           // static blockers (observe_big)
     int32_t lane_ent[GW_MAX_LANES];
     bool wg;                   // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     bool step_tb;              // step_kernel<S, 1>: TeamBattle, no blockers, one view range
@@ -3014,28 +3145,37 @@ static void set_err(const char* fmt, ...)
         }                                                                         \
     } while (0)
 
-// the parts, indexed by S / 2 (S = 1, 3, ..., 15)
-static const part_launch_fn k_part_launch[8] = {
+// the parts, indexed by S / 2 (S = 1, 3, ..., 15), then the generic one (S > 15)
+static const part_launch_fn k_part_launch[9] = {
     gw_part_launch_1, gw_part_launch_3, gw_part_launch_5, gw_part_launch_7,
-    gw_part_launch_9, gw_part_launch_11, gw_part_launch_13, gw_part_launch_15};
-static const part_attr_fn k_part_attr[8] = {
+    gw_part_launch_9, gw_part_launch_11, gw_part_launch_13, gw_part_launch_15, gw_part_launch_0};
+static const part_attr_fn k_part_attr[9] = {
     gw_part_attr_1, gw_part_attr_3, gw_part_attr_5, gw_part_attr_7,
-    gw_part_attr_9, gw_part_attr_11, gw_part_attr_13, gw_part_attr_15};
+    gw_part_attr_9, gw_part_attr_11, gw_part_attr_13, gw_part_attr_15, gw_part_attr_0};
+constexpr int FIXED_S = 2 * GW_FIXED_RANGE + 1;
+
+static int part_index(int S)
+{
+    if (S < 1 || !(S & 1) || S > 2 * GW_MAX_RANGE + 1) return -1;
+    return S > FIXED_S ? 8 : S >> 1;
+}
 
 static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const Params& p, hipStream_t st)
 {
-    if (g->S < 1 || g->S > 15 || !(g->S & 1)) return hipErrorInvalidValue;
+    const int pi = part_index(g->S);
+    if (pi < 0) return hipErrorInvalidValue;
     const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET || kind == PK_WG_COMP) ? WAVE * p.nwv : WAVE;
-    const int epw = WAVE / lane_group(g->S);        // lane_step_kernel: envs per wave
+    const int epw = g->S <= FIXED_S ? WAVE / lane_group(g->S) : 1;   // lane_step_kernel: envs per wave
     const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + epw - 1) / epw) : (unsigned)g->E;
-    return k_part_launch[g->S >> 1](kind, grid, block, smem, st, &p);
+    return k_part_launch[pi](kind, grid, block, smem, st, &p);
 }
 
 static hipError_t set_part_attrs(int S, int k0, int k1, size_t a, size_t b)
 {
-    if (S < 1 || S > 15 || !(S & 1)) return hipErrorInvalidValue;
-    hipError_t e = k_part_attr[S >> 1](k0, a);
-    return e != hipSuccess ? e : k_part_attr[S >> 1](k1, b);
+    const int pi = part_index(S);
+    if (pi < 0) return hipErrorInvalidValue;
+    hipError_t e = k_part_attr[pi](k0, a);
+    return e != hipSuccess ? e : k_part_attr[pi](k1, b);
 }
 
 static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st)
@@ -3095,7 +3235,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             set_err("agent %d view_range %d outside 0..obs_range %d", a, s.view_range, cfg->obs_range);
             return GW_E_UNSUPPORTED;
         }
-        if ((s.kind & GW_K_ATTACKING) && (s.attack_range < 0 || s.attack_range > GW_MAX_RANGE)) {
+        if ((s.kind & GW_K_ATTACKING) && (s.attack_range < 0 || s.attack_range > GW_MAX_ATTACK_RANGE)) {
             set_err("agent %d attack_range %d", a, s.attack_range);
             return GW_E_UNSUPPORTED;
         }
@@ -3185,6 +3325,14 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         return GW_E_UNSUPPORTED;
     }
     const bool wg = wg_able && (A > GW_MAX_AGENTS || cfg->force_workgroup);
+    // windows wider than the compiled parts: the generic window path of the
+    // one-wave kernels (observe_big)
+    const bool big = !pac && 2 * cfg->obs_range + 1 > FIXED_S;
+    if (big && wg) {
+        set_err("view ranges above %d run on the one-wave kernel (at most %d entities)", GW_FIXED_RANGE,
+                GW_MAX_AGENTS);
+        return GW_E_UNSUPPORTED;
+    }
     const int max_lanes = wg_able ? GW_MAX_LANES : GW_MAX_AGENTS;
     if (A == 0 || A > max_lanes) {
         set_err("%d dynamic entities outside 1..%d (%s)", A, max_lanes,
@@ -3317,11 +3465,14 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // read as dwords, so the pitch is a multiple of 4 with slack for the
     // over-read, plus one slack row at the end.  Static entities are part of
     // the template.
-    int pad = cfg->obs_range;
+    // (the generic window path bounds-checks its windows: attack ranges only)
+    int pad = big ? 0 : cfg->obs_range;
     for (int l = 0; l < A; l++)
         if ((hs[l].kind & GW_K_ATTACKING) && hs[l].attack_range > pad) pad = hs[l].attack_range;
+    const int Sst = big ? 1 : g->S;             // the observation stage's window side
     p.pad = pad;
-    p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((g->S + 3) / 4 + 1);
+    p.obs_side = g->S;
+    p.pitch = ((cfg->cols + 2 * pad + 3) / 4) * 4 + 4 * ((Sst + 3) / 4 + 1);
     p.tbl_rows = cfg->rows + 2 * pad + 1;
     {
         const size_t tb = align16((size_t)p.tbl_rows * p.pitch);
@@ -3366,10 +3517,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // blocking: shadow LUT for every range, static masks for the ranges in use
     p.blockers = any_block;
     p.lane_blockers = lane_block;
-    for (int r = 0; r <= GW_MAX_RANGE; r++) p.smask_off[r] = -1;
+    for (int r = 0; r <= GW_FIXED_RANGE; r++) p.smask_off[r] = -1;
     if (any_block) {
         std::vector<uint32_t> lut;
-        for (int r = 0; r <= GW_MAX_RANGE; r++) {
+        for (int r = 0; r <= GW_FIXED_RANGE; r++) {
             p.shadow_off[r] = (int)lut.size();
             const int D = 2 * r + 1, mw = mask_words(r);
             lut.resize(lut.size() + (size_t)D * D * mw);
@@ -3380,15 +3531,23 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         HIPCHK(hipMalloc(&g->d_shadow, lut.size() * 4));
         HIPCHK(hipMemcpy(g->d_shadow, lut.data(), lut.size() * 4, hipMemcpyHostToDevice));
         p.shadow = g->d_shadow;
-        bool used[GW_MAX_RANGE + 1] = {};
+        bool used[GW_FIXED_RANGE + 1] = {};
         for (int l = 0; l < A; l++) {
-            if (hs[l].kind & GW_K_GRID_OBSERVER) used[cfg->obs_range] = true;
+            if ((hs[l].kind & GW_K_GRID_OBSERVER) && !big) used[cfg->obs_range] = true;
             if (hs[l].kind & GW_K_ATTACKING) used[hs[l].attack_range] = true;
         }
         std::vector<int> sblock;
         for (int a : statics) if (cfg->agents[a].kind & GW_K_BLOCKING) sblock.push_back(a);
+        if (big && !sblock.empty()) {           // observe_big: the static blockers' cells
+            std::vector<int32_t> sl;
+            for (int a : sblock) sl.push_back((cfg->agents[a].init_row << 16) | cfg->agents[a].init_col);
+            HIPCHK(hipMalloc(&g->d_sblk, sl.size() * 4));
+            HIPCHK(hipMemcpy(g->d_sblk, sl.data(), sl.size() * 4, hipMemcpyHostToDevice));
+            p.sblk = g->d_sblk;
+            p.n_sblk = (int)sl.size();
+        }
         std::vector<uint32_t> sm;
-        for (int r = 0; r <= GW_MAX_RANGE && !sblock.empty(); r++) {
+        for (int r = 0; r <= GW_FIXED_RANGE && !sblock.empty(); r++) {
             if (!used[r]) continue;
             p.smask_off[r] = (int)sm.size();
             const int D = 2 * r + 1, mw = mask_words(r);
@@ -3414,14 +3573,14 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // S x S slot; the blocking LUTs are re-laid out in slot geometry per range
     for (int l = 0; l < A; l++)
         if ((hs[l].kind & GW_K_GRID_OBSERVER) && !pac && hs[l].view_range != cfg->obs_range) p.hetero_view = 1;
-    for (int r = 0; r <= GW_MAX_RANGE; r++) { p.hshadow_off[r] = -1; p.hsmask_off[r] = -1; }
+    for (int r = 0; r <= GW_FIXED_RANGE; r++) { p.hshadow_off[r] = -1; p.hsmask_off[r] = -1; }
     if (p.hetero_view && wg) {
         set_err("observers with different view ranges run on the one-wave kernel only");
         return GW_E_UNSUPPORTED;
     }
-    if (p.hetero_view && any_block) {
+    if (p.hetero_view && any_block && !big) {
         const int S = g->S, MWS = mask_words(cfg->obs_range), R = cfg->obs_range;
-        bool used[GW_MAX_RANGE + 1] = {};
+        bool used[GW_FIXED_RANGE + 1] = {};
         for (int l = 0; l < A; l++) if (hs[l].kind & GW_K_GRID_OBSERVER) used[hs[l].view_range] = true;
         // slot bits of the cells a blocker at (dr, dc) hides from a range-v window
         auto slot_shadow = [&](int v, int dr, int dc, uint32_t* out) {
@@ -3466,10 +3625,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             p.hsmask = g->d_hsmask;
         }
     }
-    p.pair_cap = (int)((work_bytes(HW, A, g->S, max_enc) - NACT_BYTES -
-                        (size_t)A * g->S * ((g->S + 3) & ~3)) / 2);
-    p.nact_off = (int32_t)(work_bytes(HW, A, g->S, max_enc) - NACT_BYTES);
-    g->smem_step = smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
+    p.pair_cap = (int)((work_bytes(HW, A, Sst, max_enc) - NACT_BYTES -
+                        (size_t)A * Sst * ((Sst + 3) & ~3)) / 2);
+    p.nact_off = (int32_t)(work_bytes(HW, A, Sst, max_enc) - NACT_BYTES);
+    g->smem_step = smem_bytes(HW, A, Sst, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
         const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE;
         const size_t wb = work_bytes(HW, A, g->S, max_enc);
@@ -3549,7 +3708,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     else if (!pac) HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
-    g->step_tb = GW_STEP_SPEC && !wg && !pac && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
+    g->step_tb = GW_STEP_SPEC && !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
                  !p.hetero_view;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));
     // MazeNavigation with the navigator and the target as its only lanes
@@ -3557,7 +3716,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // health, no blocking lane, the target a plain entity: one lane per env
     // (gw_lane.inc)
     {
-        bool able = maze && A == 2 && !pac && !wg && !p.lane_blockers && !p.hetero_view && p.nav >= 0 &&
+        bool able = maze && A == 2 && !pac && !wg && !big && !p.lane_blockers && !p.hetero_view && p.nav >= 0 &&
                     p.target >= 0 && p.nav != p.target;
         for (int l = 0; able && l < A; l++) {
             if (hs[l].init_r < 0 || hs[l].init_c < 0 || (hs[l].kind & GW_K_HEALTH)) able = false;
@@ -3569,7 +3728,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         // its LDS: padded template + static-blocker masks at the view range +
         // static-cell bits (lane_step_kernel's carve-up)
         const int S = g->S, R = S / 2, MWS = (S * S + 31) / 32;
-        const size_t nsm = (p.blockers && p.smask_off[R] >= 0) ? (size_t)HW * MWS : 0;
+        const size_t nsm = (p.blockers && R <= GW_FIXED_RANGE && p.smask_off[R] >= 0) ? (size_t)HW * MWS : 0;
         g->smem_lane = 16 * (size_t)((p.tbl_rows * p.pitch + 15) / 16) + 4 * ((nsm + 3) & ~(size_t)3) +
                        (p.static_bits ? 4 * (size_t)((HW + 31) / 32) : 0);
         const size_t static_lds = 4 * GW_MT_N;
@@ -3598,7 +3757,7 @@ gw_status gw_destroy(gw_handle g)
     (void)hipFree(g->d_static_bits); (void)hipFree(g->d_shadow); (void)hipFree(g->d_smask);
     (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
     (void)hipFree(g->d_passive); (void)hipFree(g->d_passive_enc);
-    (void)hipFree(g->d_hshadow); (void)hipFree(g->d_hsmask);
+    (void)hipFree(g->d_hshadow); (void)hipFree(g->d_hsmask); (void)hipFree(g->d_sblk);
     (void)hipFree(g->d_place_order); (void)hipFree(g->d_act_order);
     delete g;
     return GW_OK;

@@ -135,8 +135,8 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
                 if a.encoding not in attack[0].attack_mapping:
                     # the reference raises KeyError at actor.py:385 on the first candidate
                     raise UnsupportedConfig(f"{a.id}'s encoding is not in attack_mapping")
-                if a.attack_range > _abi.GW_MAX_RANGE:
-                    raise UnsupportedConfig(f"attack_range > {_abi.GW_MAX_RANGE}")
+                if a.attack_range > _abi.GW_MAX_ATTACK_RANGE:
+                    raise UnsupportedConfig(f"attack_range > {_abi.GW_MAX_ATTACK_RANGE}")
     for x in actors:
         if isinstance(x, DriftMoveActor) and program == _abi.GW_SIM_PACMAN:
             continue

@@ -104,13 +104,16 @@ class ComponentRuntime:
         self.ids = list(agents)
         # selective actions need the (2r+1)^2 action row; binary uses args[2] only
         kind = _abi.GW_ATTACK_SELECTIVE if sig[2] else _abi.GW_ATTACK_BINARY
-        # the position-centred window is capped at GW_MAX_RANGE; the absolute
-        # observer takes its view range with each call (any range)
-        views = [min(a.view_range, _abi.GW_MAX_RANGE) for a in agents.values()
+        # the position-centred window is capped at GW_MAX_RANGE (ranges above
+        # GW_FIXED_RANGE: the one-wave kernel's generic window path); without a
+        # position-centred observer the window is not used at all, and the
+        # absolute observer takes its view range with each call (any range)
+        cap = _abi.GW_MAX_RANGE if sig[4] else _abi.GW_FIXED_RANGE
+        views = [min(a.view_range, cap) for a in agents.values()
                  if isinstance(a, GridObservingAgent)]
         specs = [agent_spec(a) for a in agents.values()]
         for s_, a in zip(specs, agents.values()):
-            s_.view_range = min(s_.view_range, _abi.GW_MAX_RANGE)
+            s_.view_range = min(s_.view_range, cap)
             if not sig[4] and s_.kind & _abi.GW_K_GRID_OBSERVER:
                 # no position-centred window on this grid: one view range
                 # (the absolute observer takes its own with each call)

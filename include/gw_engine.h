@@ -75,8 +75,11 @@ extern "C" {
                                 entity (BASELINE config 4: 256 entities)      */
 #define GW_MAX_ENTITIES 4096 /* lanes + static entities                       */
 #define GW_MAX_ENC      15   /* encodings 1..15                               */
-#define GW_MAX_CELLS  4096   /* rows*cols                                     */
-#define GW_MAX_RANGE     7   /* view / attack range                           */
+#define GW_MAX_CELLS 16384   /* rows*cols (and the LDS budget: 160 KiB per env) */
+#define GW_MAX_RANGE    64   /* view range (windows up to 129x129; ranges above 7
+                                run on the generic window path of the one-wave
+                                kernel)                                        */
+#define GW_MAX_ATTACK_RANGE 7 /* attack range                                 */
 #define GW_ACT_DIM       3   /* binary-attack sims: actions[e][a] = {move_row, move_col, attack};
                                 see gw_act_dim() for the general width                */
 #define GW_MT_N        624   /* MT19937 state words                           */

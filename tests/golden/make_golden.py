@@ -116,6 +116,13 @@ CASES = [
          n_steps=120, horizon=40, seed_base=27, corners=True,
          runner=dict(move_range=2, view_range=3, initial_health=1),
          target=dict(view_range=7, attack_range=1, attack_strength=1, attack_accuracy=1)),
+    # the same example's layout at 16x16 with its own view-range rule
+    # (rllib_reach_the_target.py:22-31: runners grid_size / 2, the target
+    # grid_size): windows of 17x17 and 33x33 cells
+    dict(name='rtt_16_example', kind='rtt', rows=16, cols=16, n_barriers=10, n_runners=4, n_envs=3,
+         n_steps=100, horizon=40, seed_base=29, corners=True,
+         runner=dict(move_range=2, view_range=8, initial_health=1),
+         target=dict(view_range=16, attack_range=1, attack_strength=1, attack_accuracy=1)),
     # TeamBattle with view ranges 1, 2 and 3 mixed, blocking walls and fighters
     dict(name='tb_views', rows=10, cols=10, n_agents=18, n_teams=2, n_envs=4, n_steps=120,
          horizon=60, seed_base=81, views=[1, 3, 2], walls=[[2, c] for c in range(2, 7)] +
