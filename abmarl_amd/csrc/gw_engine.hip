@@ -274,6 +274,26 @@ __device__ __forceinline__ void buf_store_i8x4(__amdgpu_buffer_rsrc_t rs, uint32
 #endif
 }
 
+// The kernel's Params (its only / first argument, at kernarg offset 0) read
+// afresh: the kernarg segment pointer passed through an empty asm, so loads
+// of its fields after this point cannot be hoisted above it.  A step loop
+// calls it once per iteration: the fields become scalar loads from the
+// kernarg segment (scalar cache) at their use instead of loop-invariant
+// values -- and the 64-bit lane masks of every loop-invariant config test --
+// held live across the loop, which overflow the SGPR file and spill into
+// VGPR lanes (a v_writelane / v_readlane pair per reload, VALU work).
+#ifndef GW_FRESH_PARAMS
+#define GW_FRESH_PARAMS 1
+#endif
+struct Params;
+__device__ __forceinline__ const Params& kernel_params()
+{
+    typedef const __attribute__((address_space(4))) Params KParams;
+    KParams* q = (KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return *(const Params*)q;
+}
+
 __device__ __forceinline__ double rld(double v, int l)
 {
     uint64_t b = __double_as_longlong(v);
@@ -2189,6 +2209,10 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_PREFETCH_ACTIONS
 #define GW_PREFETCH_ACTIONS 1
 #endif
+// lane_step_kernel: steps of actions in flight ahead of the step (gw_lane.inc)
+#ifndef GW_LANE_PD
+#define GW_LANE_PD 4
+#endif
 #ifndef GW_STEP_SPEC
 #define GW_STEP_SPEC 1
 #endif
@@ -2240,6 +2264,9 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     int pa0 = 0, pa1 = 0, pa2 = 0;             // actions of step t + 1 (prefetched)
     bool nact_ok = false;                       // sm.nact holds them
     for (int t = 0; t < p.nsteps; t++) {
+#if GW_FRESH_PARAMS
+        const Params& p = kernel_params();
+#endif
         // progress priority (gw_rollout): the four envs of a SIMD start
         // together, and VALU issue goes by priority, then age, so the youngest
         // wave would trail the others and end the launch alone; a wave drops
