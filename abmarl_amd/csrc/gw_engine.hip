@@ -3207,7 +3207,14 @@ static hipError_t set_part_attrs(int S, int k0, int k1, size_t a, size_t b)
 
 static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(pac_kernel, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    // the step protocols' own instantiations (the other modes' code and its
+    // registers out of the step loop); resets and the dict API: the generic one
+    if (p.mode == PAC_STEP_TURN)
+        hipLaunchKernelGGL(pac_kernel<PAC_STEP_TURN>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    else if (p.mode == PAC_STEP_ALL)
+        hipLaunchKernelGGL(pac_kernel<PAC_STEP_ALL>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    else
+        hipLaunchKernelGGL(pac_kernel<-1>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
     return hipGetLastError();
 }
 
@@ -3657,7 +3664,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.nact_off = (int32_t)(work_bytes(HW, A, Sst, max_enc) - NACT_BYTES);
     g->smem_step = smem_bytes(HW, A, Sst, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
-        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE;
+        // pac_carve: cval | pb | clist | cp | penc
+        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
+                          align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS;
         const size_t wb = work_bytes(HW, A, g->S, max_enc);
         if (pw > wb) g->smem_step += pw - wb;
     }
@@ -3724,7 +3733,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         HIPCHK(hipMemset(p.pbits, 0, pwn * 4));
         HIPCHK(hipMalloc(&p.cyc, (size_t)n_envs * 4));
         HIPCHK(hipMemset(p.cyc, 0xff, (size_t)n_envs * 4));      // -1: no turn yet
-        HIPCHK(hipFuncSetAttribute((const void*)pac_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        HIPCHK(hipFuncSetAttribute((const void*)pac_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)g->smem_step));
+        HIPCHK(hipFuncSetAttribute((const void*)pac_kernel<PAC_STEP_TURN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)g->smem_step));
+        HIPCHK(hipFuncSetAttribute((const void*)pac_kernel<PAC_STEP_ALL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)g->smem_step));
     }
     HIPCHK(hipMalloc(&p.racc, EA * sizeof(double)));
