@@ -3037,7 +3037,10 @@ __global__ void random_actions_kernel(PolicySpec ps, int E, int A, uint64_t key,
 // parts in parallel and links them with the host part).  Each part exports a
 // launcher and an attribute setter; the host part dispatches on S to them.
 enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK_COMP = 4, PK_STEP_TB = 5, PK_STEP_LANE = 6,
-                  PK_WG_COMP = 7 };
+                  PK_WG_COMP = 7, PK_STEP_LANE_NS = 8 };
+// lane_step_kernel's instantiation for the rollout protocol (next-step
+// auto-reset, skip_done_obs, no persistent obs buffer): its flags at compile time
+#define LANE_FL_NS (2 | (1 << 3))
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
@@ -3075,6 +3078,7 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
     case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_COMP: hipLaunchKernelGGL(comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     case PK_STEP_LANE: hipLaunchKernelGGL(lane_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP_LANE_NS: hipLaunchKernelGGL((lane_step_kernel<S, LANE_FL_NS>), dim3(grid), dim3(block), smem, st, p); break;
     case PK_WG_COMP: hipLaunchKernelGGL(wg_comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
     default: return hipErrorInvalidValue;
     }
@@ -3098,6 +3102,7 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
                   : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
                   : kind == PK_COMP ? (const void*)comp_kernel<S>
                   : kind == PK_STEP_LANE ? (const void*)lane_step_kernel<S>
+                  : kind == PK_STEP_LANE_NS ? (const void*)lane_step_kernel<S, LANE_FL_NS>
                   : kind == PK_WG_COMP ? (const void*)wg_comp_kernel<S>
                                        : (const void*)wg_reset_kernel<S>;
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -3193,7 +3198,8 @@ static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const P
     if (pi < 0) return hipErrorInvalidValue;
     const unsigned block = (kind == PK_WG_STEP || kind == PK_WG_RESET || kind == PK_WG_COMP) ? WAVE * p.nwv : WAVE;
     const int epw = g->S <= FIXED_S ? WAVE / lane_group(g->S) : 1;   // lane_step_kernel: envs per wave
-    const unsigned grid = kind == PK_STEP_LANE ? (unsigned)((g->E + epw - 1) / epw) : (unsigned)g->E;
+    const unsigned grid = (kind == PK_STEP_LANE || kind == PK_STEP_LANE_NS) ? (unsigned)((g->E + epw - 1) / epw)
+                                                                           : (unsigned)g->E;
     return k_part_launch[pi](kind, grid, block, smem, st, &p);
 }
 
@@ -3221,7 +3227,10 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 static hipError_t do_step(const gw_engine* g, Params& p, hipStream_t st)
 {
     if (g->pacman) { p.mode = PAC_STEP_ALL; return launch_pac(g, p, st); }
-    if (g->lane_envs) return part_launch(g, PK_STEP_LANE, g->smem_lane, p, st);
+    if (g->lane_envs) {
+        const bool ns = p.autoreset == 2 && p.skip_done_obs && !p.persistent_obs;
+        return part_launch(g, ns ? PK_STEP_LANE_NS : PK_STEP_LANE, g->smem_lane, p, st);
+    }
     // an action order other than the agents dict's runs on the generic kernel
     const bool tb = g->step_tb && !p.act_order;
     return part_launch(g, g->wg ? PK_WG_STEP : (tb ? PK_STEP_TB : PK_STEP), g->smem_step, p, st);
@@ -3782,7 +3791,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         }
         g->lane_envs = able && cfg->env_per_lane >= 0;
         g->lane_envs_config = g->lane_envs;
-        if (g->lane_envs) HIPCHK(set_part_attrs(g->S, PK_STEP_LANE, PK_STEP_LANE, g->smem_lane, g->smem_lane));
+        if (g->lane_envs) HIPCHK(set_part_attrs(g->S, PK_STEP_LANE, PK_STEP_LANE_NS, g->smem_lane, g->smem_lane));
     }
     *out = g;
     return GW_OK;

@@ -307,7 +307,7 @@ WORKLOADS = {
     # name: (builder, default envs per GPU, step-kernel name, description)
     'team_battle': (team_battle_sim, 4096, 'step_kernel<7, 1>',
                     'TeamBattle 32x32, 64 agents / 2 teams'),
-    'maze': (maze_sim, 1024, 'lane_step_kernel<5>',
+    'maze': (maze_sim, 1024, 'lane_step_kernel<5, 10>',
              'MazeNavigation 16x16 (BASELINE config 2), 1 navigator, blocking walls'),
     'rtt': (rtt_sim, 1024, 'wg_step_kernel<7>',
             'ReachTheTarget 64x64 (BASELINE config 4), 256 entities'),

@@ -22,7 +22,7 @@ import json
 import os
 import shutil
 
-KERNEL = {'team_battle': 'step_kernel<7, 1>', 'rtt': 'wg_step_kernel<7>', 'maze': 'lane_step_kernel<5>'}
+KERNEL = {'team_battle': 'step_kernel<7, 1>', 'rtt': 'wg_step_kernel<7>', 'maze': 'lane_step_kernel<5, 10>'}
 
 
 def find(root, pattern):
