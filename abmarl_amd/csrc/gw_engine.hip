@@ -249,10 +249,6 @@ __device__ __forceinline__ bool rlb(bool v, int l) { return __builtin_amdgcn_rea
 #ifndef GW_OBS_STORE_AUX
 #define GW_OBS_STORE_AUX 2
 #endif
-// observe_fixed: rows left unwritten -> only the written rows' dwords stored
-#ifndef GW_OBS_COMPACT_STORE
-#define GW_OBS_COMPACT_STORE 0
-#endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // four observation bytes (valid values >= -2, 0x80 = skipped) -> four int32
 // max(sext(byte), -2) with SDWA byte selects (one VALU per output), stored
@@ -458,6 +454,46 @@ __device__ __forceinline__ void mt_twist(uint32_t* key)
     }
 }
 
+// The twist of a draw that crosses the key's end, as ONE out-of-line copy:
+// Rng::next is inlined at every draw site, and a full twist loop at each of
+// them made the kernels several times larger than the instruction cache.
+// The key pointer is an LDS (address space 3) one, so the callee's accesses
+// stay ds_* operations.
+#ifndef GW_TWIST_CALL
+#define GW_TWIST_CALL 1
+#endif
+__device__ __noinline__ void mt_twist_call(__attribute__((address_space(3))) uint32_t* key)
+{
+    const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
+    const int l = lane_id();
+    __builtin_amdgcn_wave_barrier();
+    for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
+        const int i = b + l;
+        uint32_t nv = 0;
+        if (i < GW_MT_N - 1) {
+            const uint32_t y = (key[i] & UP) | (key[i + 1] & LO);
+            int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
+            nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (i < GW_MT_N - 1) key[i] = nv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
+    const uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (l == 0) key[GW_MT_N - 1] = nv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // numpy legacy RandomState (mt19937.c).  The 624-word key stays in HBM until
 // a draw needs it (a word outside the cached block, a twist, a reset); it is
 // then copied to LDS.  The 64 tempered words from the stream position are
@@ -492,7 +528,11 @@ struct Rng {
     __device__ __forceinline__ void twist()
     {
         ensure_key();
+#if GW_TWIST_CALL
+        mt_twist_call((__attribute__((address_space(3))) uint32_t*)key);
+#else
         mt_twist(key);
+#endif
         pos = 0;
         base = -1;
         dirty = true;
@@ -1171,48 +1211,6 @@ __device__ __forceinline__ void observe_fixed(const Params& p, int e, Smem& sm, 
     const int total = A * SS;
     int32_t* out = obs + (size_t)e * total;
     const uint32_t* cs = (const uint32_t*)sm.stage;
-#if GW_OBS_COMPACT_STORE
-    if (skip) {
-        // Rows left unwritten (skip_done_obs / persistent_obs): only the
-        // written rows go out, one dword per lane per store.  The written
-        // rows in lane order form a stream of n * SS dwords; stream position
-        // m is row rank m / SS, whose lane comes from a permute of the row
-        // lanes by rank, and stage byte lane * SS + m % SS.  A dword store
-        // costs the CU's store path a quarter of a dwordx4 store, and only
-        // ceil(n SS / 64) of them are issued instead of the full
-        // ceil(A SS / 256) dwordx4 stores with the skipped dwords dropped.
-        const uint64_t vmask = A >= WAVE ? ~0ull : ((1ull << A) - 1ull);
-        const uint64_t wr = vmask & ~skip;
-        const int n = __popcll(wr);
-        const int T = n * SS;
-        const bool w_me = (wr >> l) & 1ull;
-        const int rk_w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wr, 0u));
-        const int rk = w_me ? rk_w : n + (l - rk_w);           // a permutation of the lanes
-        const int lane_of_rank = __builtin_amdgcn_ds_permute(rk * 4, l);
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, total * 4, BUF_RSRC_W3);
-        constexpr int U = 4;
-        for (int m0 = 0; m0 < T; m0 += U * WAVE) {
-            int a[U], c[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int m = m0 + u * WAVE + l;
-                const int r = m / SS;
-                c[u] = m - r * SS;
-                a[u] = __builtin_amdgcn_ds_bpermute(r * 4, lane_of_rank) & (WAVE - 1);
-            }
-            int v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) v[u] = sm.stage[a[u] * SS + c[u]];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int m = m0 + u * WAVE + l;
-                __builtin_amdgcn_raw_buffer_store_b32(v[u], rs, m < T ? (a[u] * SS + c[u]) * 4 : BUF_OOB, 0,
-                                                      GW_OBS_STORE_AUX);
-            }
-        }
-        return;
-    }
-#endif
     if ((total & 3) == 0) {
         // raw buffer stores on the env's obs row: the range check drops the
         // tail past A*SS (no per-store bound test) and a skipped dword is sent

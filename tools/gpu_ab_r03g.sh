@@ -11,5 +11,3 @@ for L in libgw_engine.so libgw_engine_pacq.so libgw_engine.so libgw_engine_pacq.
       > gpurun_out/g_pac.log 2>&1 || { tail -20 gpurun_out/g_pac.log; exit 1; }
   echo "{\"lib\": \"$L\", \"line\": $(grep '^{' gpurun_out/g_pac.log)}" >> gpurun_out/ab_g.jsonl
 done
-timeout -k 10 300 python3 tools/ab_headline.py $B/libgw_engine.so $B/libgw_engine_nogst.so $B/libgw_engine.so $B/libgw_engine_nogst.so \
-    > gpurun_out/ab_head_g.jsonl 2> gpurun_out/ab_head_g.err
