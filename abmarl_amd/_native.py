@@ -44,6 +44,7 @@ SIGNATURES = {
     'gw_rollout_step': (_i32, [_vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
                                _vp, _vp]),
     'gw_rollout': (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    'gw_set_launch_events': (_i32, [_vp, _vp, _vp]),
     'gw_component': (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     'gw_generate_maze': (_i32, [_vp, _vp, _vp, _vp]),
     'gw_destroy': (_i32, [_vp]),

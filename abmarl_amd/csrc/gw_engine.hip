@@ -37,6 +37,7 @@
 //   mt[E][704] u32 (key[624], pos @624, seq counter @625, cached block base
 //   @626, 64 tempered words from it @640), steps[E] i32.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -3086,44 +3087,52 @@ enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK
 // auto-reset, skip_done_obs, no persistent obs buffer): its flags at compile time
 #define LANE_FL_NS (2 | (1 << 3))
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
-                                     hipStream_t st, const void* params);
+                                     hipStream_t st, const void* params, hipEvent_t ev0, hipEvent_t ev1);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
 #define GW_PART_CAT2(a, b) a##b
 #define GW_PART_CAT(a, b) GW_PART_CAT2(a, b)
 #define GW_PART_DECL(S_)                                                                      \
     hipError_t GW_PART_CAT(gw_part_launch_, S_)(int, unsigned, unsigned, size_t, hipStream_t, \
-                                                const void*);                                 \
+                                                const void*, hipEvent_t, hipEvent_t);         \
     hipError_t GW_PART_CAT(gw_part_attr_, S_)(int, size_t);
 GW_PART_DECL(1) GW_PART_DECL(3) GW_PART_DECL(5) GW_PART_DECL(7)
 GW_PART_DECL(9) GW_PART_DECL(11) GW_PART_DECL(13) GW_PART_DECL(15)
 GW_PART_DECL(0)   // the generic window path: S at run time (> 2 * GW_FIXED_RANGE + 1)
 
 #ifdef GW_PART_S
+// ev0 / ev1 (gw_set_launch_events): the kernel's own start / end timestamps
+// (hipExtLaunchKernel), no separate event records around the launch
+#define GW_LAUNCH(K)                                                                          \
+    do {                                                                                      \
+        if (ev0) hipExtLaunchKernelGGL(K, dim3(grid), dim3(block), (uint32_t)smem, st, ev0, ev1, 0, p); \
+        else hipLaunchKernelGGL(K, dim3(grid), dim3(block), smem, st, p);                     \
+    } while (0)
 hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsigned block, size_t smem,
-                                                   hipStream_t st, const void* params)
+                                                   hipStream_t st, const void* params, hipEvent_t ev0,
+                                                   hipEvent_t ev1)
 {
     const Params& p = *static_cast<const Params*>(params);
 #if GW_PART_S == 0
     // the generic window path: the one-wave step / reset / component kernels
     switch (kind) {
-    case PK_STEP: hipLaunchKernelGGL((step_kernel<0, 0>), dim3(grid), dim3(block), smem, st, p); break;
-    case PK_RESET: hipLaunchKernelGGL(reset_kernel<0>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_COMP: hipLaunchKernelGGL(comp_kernel<0>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP: GW_LAUNCH((step_kernel<0, 0>)); break;
+    case PK_RESET: GW_LAUNCH((reset_kernel<0>)); break;
+    case PK_COMP: GW_LAUNCH((comp_kernel<0>)); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 #else
     constexpr int S = GW_PART_S;
     switch (kind) {
-    case PK_STEP: hipLaunchKernelGGL((step_kernel<S, 0>), dim3(grid), dim3(block), smem, st, p); break;
-    case PK_STEP_TB: hipLaunchKernelGGL((step_kernel<S, 1>), dim3(grid), dim3(block), smem, st, p); break;
-    case PK_RESET: hipLaunchKernelGGL(reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_WG_STEP: hipLaunchKernelGGL(wg_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_WG_RESET: hipLaunchKernelGGL(wg_reset_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_COMP: hipLaunchKernelGGL(comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_STEP_LANE: hipLaunchKernelGGL(lane_step_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
-    case PK_STEP_LANE_NS: hipLaunchKernelGGL((lane_step_kernel<S, LANE_FL_NS>), dim3(grid), dim3(block), smem, st, p); break;
-    case PK_WG_COMP: hipLaunchKernelGGL(wg_comp_kernel<S>, dim3(grid), dim3(block), smem, st, p); break;
+    case PK_STEP: GW_LAUNCH((step_kernel<S, 0>)); break;
+    case PK_STEP_TB: GW_LAUNCH((step_kernel<S, 1>)); break;
+    case PK_RESET: GW_LAUNCH((reset_kernel<S>)); break;
+    case PK_WG_STEP: GW_LAUNCH((wg_step_kernel<S>)); break;
+    case PK_WG_RESET: GW_LAUNCH((wg_reset_kernel<S>)); break;
+    case PK_COMP: GW_LAUNCH((comp_kernel<S>)); break;
+    case PK_STEP_LANE: GW_LAUNCH((lane_step_kernel<S>)); break;
+    case PK_STEP_LANE_NS: GW_LAUNCH((lane_step_kernel<S, LANE_FL_NS>)); break;
+    case PK_WG_COMP: GW_LAUNCH((wg_comp_kernel<S>)); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3156,6 +3165,8 @@ hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
 
 // ====================================================================== C-ABI
 struct gw_engine {
+    // gw_set_launch_events: start / end events of the next step launch
+    mutable hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int device;
     int E, A, H, W, S, max_enc;
     Params base;
@@ -3244,7 +3255,10 @@ static hipError_t part_launch(const gw_engine* g, int kind, size_t smem, const P
     const int epw = g->S <= FIXED_S ? WAVE / lane_group(g->S) : 1;   // lane_step_kernel: envs per wave
     const unsigned grid = (kind == PK_STEP_LANE || kind == PK_STEP_LANE_NS) ? (unsigned)((g->E + epw - 1) / epw)
                                                                            : (unsigned)g->E;
-    return k_part_launch[pi](kind, grid, block, smem, st, &p);
+    // the events of gw_set_launch_events go to the next launch only
+    const hipEvent_t ev0 = g->ev0, ev1 = g->ev1;
+    g->ev0 = g->ev1 = nullptr;
+    return k_part_launch[pi](kind, grid, block, smem, st, &p, ev0, ev1);
 }
 
 static hipError_t set_part_attrs(int S, int k0, int k1, size_t a, size_t b)
@@ -3259,12 +3273,15 @@ static hipError_t launch_pac(const gw_engine* g, const Params& p, hipStream_t st
 {
     // the step protocols' own instantiations (the other modes' code and its
     // registers out of the step loop); resets and the dict API: the generic one
-    if (p.mode == PAC_STEP_TURN)
-        hipLaunchKernelGGL(pac_kernel<PAC_STEP_TURN>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
-    else if (p.mode == PAC_STEP_ALL)
-        hipLaunchKernelGGL(pac_kernel<PAC_STEP_ALL>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
-    else
-        hipLaunchKernelGGL(pac_kernel<-1>, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    const hipEvent_t ev0 = g->ev0, ev1 = g->ev1;          // gw_set_launch_events: this launch only
+    g->ev0 = g->ev1 = nullptr;
+    auto go = [&](auto kernel) {
+        if (ev0) hipExtLaunchKernelGGL(kernel, dim3(g->E), dim3(WAVE), (uint32_t)g->smem_step, st, ev0, ev1, 0, p);
+        else hipLaunchKernelGGL(kernel, dim3(g->E), dim3(WAVE), g->smem_step, st, p);
+    };
+    if (p.mode == PAC_STEP_TURN) go(pac_kernel<PAC_STEP_TURN>);
+    else if (p.mode == PAC_STEP_ALL) go(pac_kernel<PAC_STEP_ALL>);
+    else go(pac_kernel<-1>);
     return hipGetLastError();
 }
 
@@ -4280,6 +4297,14 @@ gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32
     p.nsteps = n_steps; p.ad_in = all_done_in; p.skip_done_obs = skip_done_obs != 0;
     p.ad_out = all_done_in;                // each env's wave reads it first, writes it last
     HIPCHK(do_step(g, p, st));
+    return GW_OK;
+}
+
+gw_status gw_set_launch_events(gw_handle g, void* start_event, void* stop_event)
+{
+    if (!g || (start_event == nullptr) != (stop_event == nullptr)) return GW_E_INVALID;
+    g->ev0 = (hipEvent_t)start_event;
+    g->ev1 = (hipEvent_t)stop_event;
     return GW_OK;
 }
 

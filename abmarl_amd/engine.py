@@ -228,7 +228,25 @@ class GridWorldEngine:
         self._check_debug('gw_turn_rollout')
         return out
 
-    def turn_rollout_launcher(self, actions, horizon=0, out=None):
+    def _event_setter(self, events):
+        """events = (start, stop) torch.cuda.Events already recorded once (so
+        their hipEvents exist): a callable that hands them to the next kernel
+        launch (gw_set_launch_events), which records them as part of its own
+        dispatch instead of two event records around the launch."""
+        if events is None:
+            return None
+        a, b = events
+        ha, hb = int(a.cuda_event), int(b.cuda_event)
+        assert ha and hb, "launch events must have been recorded once (created)"
+        fn, h, pa, pb = self.L.gw_set_launch_events, self.h, C.c_void_p(ha), C.c_void_p(hb)
+
+        def arm():
+            st = fn(h, pa, pb)
+            if st != 0:
+                _native.check(st, 'gw_set_launch_events')
+        return arm
+
+    def turn_rollout_launcher(self, actions, horizon=0, out=None, events=None):
         """A prepared gw_turn_rollout launch (see rollout_launcher); the
         single-call turn buffer is not refreshed by it."""
         K = int(actions.shape[0])
@@ -242,8 +260,11 @@ class GridWorldEngine:
                 _ptr(out['all_done']), _ptr(self.all_done), _ptr(out['returned']), _ptr(out['turn']),
                 _ptr(self.acting), int(horizon), _ptr(self.err), _stream())
         keep = (actions, out)
+        arm = self._event_setter(events)
 
         def launch():
+            if arm is not None:
+                arm()
             st = fn(*args)
             if st != 0:
                 _native.check(st, 'gw_turn_rollout')
@@ -455,12 +476,15 @@ class GridWorldEngine:
         self._check_debug('gw_rollout')
         return out
 
-    def rollout_launcher(self, actions, horizon=0, autoreset='next_step', skip_done_obs=False, out=None):
+    def rollout_launcher(self, actions, horizon=0, autoreset='next_step', skip_done_obs=False, out=None,
+                         events=None):
         """A prepared gw_rollout launch: the arguments of rollout(actions, ...)
         are validated and built once, on the current stream, and the returned
         zero-argument callable launches exactly that fragment with one ctypes
         call (a training loop re-launching the same slabs, or a benchmark's
-        timed region).  It keeps references to `actions` and `out`."""
+        timed region).  It keeps references to `actions` and `out`.  With
+        events=(start, stop), every launch records them as part of its kernel
+        dispatch (gw_set_launch_events)."""
         K = int(actions.shape[0])
         assert actions.dtype == torch.int32 and actions.is_contiguous()
         assert tuple(actions.shape[1:]) == tuple(self.actions.shape), actions.shape
@@ -474,8 +498,11 @@ class GridWorldEngine:
                 _ptr(out['all_done']), _ptr(self.all_done), _ptr(self.acting), int(horizon),
                 self.AUTORESET_MODES[autoreset], int(bool(skip_done_obs)), _ptr(self.err), _stream())
         keep = (actions, out)
+        arm = self._event_setter(events)
 
         def launch():
+            if arm is not None:
+                arm()
             st = fn(*args)
             if st != 0:
                 _native.check(st, 'gw_rollout')

@@ -497,25 +497,28 @@ def main():
             if k == len(sizes) - 2:
                 torch.cuda.synchronize()
                 eng.check_errors(allow=allow)
-        # prepared launches (validated here, one ctypes call each when timed)
-        # and their events, created by a first record outside the timed region
-        launches = [eng.turn_rollout_launcher(all_acts[i:i + f], horizon=args.horizon, out=out) if turn
-                    else eng.rollout_launcher(all_acts[i:i + f], horizon=args.horizon, autoreset=mode,
-                                              skip_done_obs=True, out=out) for i, f in frags]
+        # prepared launches (validated here, one ctypes call each when timed);
+        # their events, created by a first record outside the timed region,
+        # are recorded by each launch's own kernel dispatch (its start and
+        # end timestamps, gw_set_launch_events): no event record call inside
+        # the timed region
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in frags]
         for a_, b_ in evs:
             a_.record()
             b_.record()
+        launches = [eng.turn_rollout_launcher(all_acts[i:i + f], horizon=args.horizon, out=out, events=ev)
+                    if turn else
+                    eng.rollout_launcher(all_acts[i:i + f], horizon=args.horizon, autoreset=mode,
+                                         skip_done_obs=True, out=out, events=ev)
+                    for (i, f), ev in zip(frags, evs)]
         acting0 = eng.acting.clone()                      # after the last warmup fragment
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for launch, ev in zip(launches, evs):
-            ev[0].record()
+        for launch in launches:
             launch()
-            ev[1].record()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -587,8 +590,9 @@ def main():
         roof = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                 'traffic': traffic, 'kernel': kname, 'kernel_ms': round(step_ms_all, 4),
-                'kernel_timing': (f'HIP events around every gw_rollout launch ({F} steps) on the launch '
-                                  f'stream, mean; max over ranks' if rollout else
+                'kernel_timing': (f'HIP events recorded by every gw_rollout launch\'s own kernel dispatch '
+                                  f'(hipExtLaunchKernel start/stop, {F} steps) on the launch stream, mean; '
+                                  f'max over ranks' if rollout else
                                   f'HIP events around the step kernel of every {max(1, args.event_every)}'
                                   f'-th timed step (launch stream), mean; max over ranks'),
                 'steps_per_launch': F,

@@ -432,6 +432,16 @@ gw_status gw_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32
                      int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
                      void* stream);
 
+/* Timing hook (no reference counterpart: instrumentation of the launch the
+   reference's step loop is timed around).  The NEXT kernel launch of the
+   handle's step / reset kernels (gw_step*, gw_rollout, gw_rollout_step's
+   step, gw_turn_step, gw_turn_rollout, gw_reset ...) records start_event
+   when its kernel starts and stop_event when it ends,
+   as part of the kernel dispatch (hipExtLaunchKernel), so a timed region
+   needs no event record calls around the launch; the events (hipEvent_t,
+   created by the caller) are cleared by that launch.  Both NULL: clear.   */
+gw_status gw_set_launch_events(gw_handle h, void* start_event, void* stop_event);
+
 /* One step of a synthetic random-policy rollout in one call: gw_random_actions
    into `actions`, then on the same stream gw_step (autoreset 0),
    gw_step_autoreset (1) or gw_step_autoreset_next (2) on those actions.  The
