@@ -2251,8 +2251,10 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_PROGRESS_PRIO
 #define GW_PROGRESS_PRIO 1
 #endif
+// next-step actions loaded ahead and parked in LDS: measured 2 % slower per
+// 100-step fragment on the round-3 kernel (profiles/r03/ab_head_prefetch.jsonl)
 #ifndef GW_PREFETCH_ACTIONS
-#define GW_PREFETCH_ACTIONS 1
+#define GW_PREFETCH_ACTIONS 0
 #endif
 // lane_step_kernel: steps of actions in flight ahead of the step (gw_lane.inc)
 #ifndef GW_LANE_PD
