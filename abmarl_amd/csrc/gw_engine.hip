@@ -2248,8 +2248,14 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_STEP_WAVES_PER_EU
 #define GW_STEP_WAVES_PER_EU 4
 #endif
+#ifndef GW_PRIO_RESET_W
+#define GW_PRIO_RESET_W 192
+#endif
+// issue priority of a step kernel wave in gw_rollout: 1 by progress through
+// the fragment, 2 by remaining work (measured +2.8 % on the driver's
+// command, profiles/r03/ab_prio_remaining_work.jsonl)
 #ifndef GW_PROGRESS_PRIO
-#define GW_PROGRESS_PRIO 1
+#define GW_PROGRESS_PRIO 2
 #endif
 // next-step actions loaded ahead and parked in LDS: measured 2 % slower per
 // 100-step fragment on the round-3 kernel (profiles/r03/ab_head_prefetch.jsonl)
@@ -2320,7 +2326,19 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         // one level per quarter of the fragment it has done, so the SIMD's
         // waves stay within about a quarter of each other
         int prio = 0;
-        if (GW_PROGRESS_PRIO && p.nsteps > 1) prio = 3 - min(3, (4 * t) / p.nsteps);
+        if (GW_PROGRESS_PRIO == 1 && p.nsteps > 1) prio = 3 - min(3, (4 * t) / p.nsteps);
+        if (GW_PROGRESS_PRIO == 2 && p.nsteps > 1) {
+            // remaining-work priority: the wave's remaining agent-steps in this
+            // fragment (live agents x steps left, a pending horizon reset
+            // counted as GW_PRIO_RESET_W agent-steps) against a typical env's
+            // (~24 live agents): the SIMD issues the heaviest env first
+            const int left = p.nsteps - t;
+            const int nlive = __popcll(__ballot(valid && L.live));
+            const bool rpend = p.horizon > 0 && steps + left >= p.horizon;
+            const int rem = left * nlive + (rpend ? GW_PRIO_RESET_W : 0);
+            const int typ = left * 24;
+            prio = rem * 4 >= typ * 6 ? 3 : (rem * 8 >= typ * 9 ? 2 : (rem * 4 >= typ * 3 ? 1 : 0));
+        }
         set_prio(prio);
         STAMP(50);
         const int32_t* act_t = p.actions + (size_t)t * EA * p.act_dim;
