@@ -51,6 +51,7 @@ GW_K_BLOCKING = 0x40
 GW_K_ORIENTATION = 0x100
 GW_K_FOOD = 0x200
 GW_K_LANE = 0x400
+GW_K_AMMO = 0x800
 
 GW_SIM_TEAM_BATTLE = 1
 GW_SIM_MAZE_NAV = 2
@@ -95,6 +96,7 @@ class AgentSpec(C.Structure):
         ("initial_orientation", C.c_int32),
         ("done_target", C.c_int32),
         ("destroy_target", C.c_int32),
+        ("initial_ammo", C.c_int32),
     ]
 
     def __init__(self, *args, **kwargs):

@@ -65,6 +65,8 @@ SIGNATURES = {
     'gw_sim_step': (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'gw_observe': (_i32, [_vp, _i32, _vp, _vp]),
     'gw_get_aux_state': (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    'gw_get_ammo': (_i32, [_vp, _vp, _vp]),
+    'gw_set_ammo': (_i32, [_vp, _vp, _vp]),
     'gw_set_aux_state': (_i32, [_vp, _vp, _vp, _vp, _vp]),
     'gw_last_error': (C.c_char_p, []),
     'gw_abi_version': (_i32, []),

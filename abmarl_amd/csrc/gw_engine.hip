@@ -114,11 +114,13 @@ struct DevAgent {               // per-entity constants (spec table in HBM)
     // the target's lane, -1 not mapped, -2 a static entity (at tgt_pos =
     // row << 16 | col, always active)
     int32_t tgt_lane, tgt_pos, dtgt_lane;
+    int32_t init_ammo;          // AmmoAgent.initial_ammo (GW_K_AMMO)
 };
 
 struct Params {
     // engine state
     int2* pos; double* health; uint8_t* flags; uint32_t* seq; uint32_t* mt; int32_t* steps;
+    int32_t* ammo;                         // [E][A] AmmoAgent.ammo (0 for other lanes)
     const DevAgent* spec;
     // I/O
     const int32_t* actions; int32_t* obs; double* reward; uint8_t* done; uint8_t* all_done;
@@ -598,8 +600,12 @@ struct Lane {
     int r, c; uint32_t seq; double health; bool in_grid, live, active;
     bool obs_m2;         // F_OBS_M2: the persistent obs row already holds -2
     double reward;
+    int ammo;            // AmmoAgent.ammo
 };
 
+// AMMO: the lane's AmmoAgent.ammo too (the TeamBattle instantiation of the
+// step kernel, whose configs hold no AmmoAgent, leaves it out)
+template <bool AMMO = true>
 __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool valid)
 {
     // unconditional loads (lanes past A read lane 0's row), then selects: a
@@ -612,6 +618,7 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
     const uint32_t sq = p.seq[k];
     const double h = p.health[k];
     const uint8_t f = p.flags[k];
+    const int32_t am = AMMO ? p.ammo[k] : 0;
     L.enc = valid ? s.enc : 0; L.kind = valid ? s.kind : 0u;
     L.view = valid ? s.view_range : 0; L.mrange = valid ? s.move_range : 0;
     L.arange = valid ? s.attack_range : 0; L.simul = valid ? s.simul : 0;
@@ -626,8 +633,10 @@ __device__ __forceinline__ void load_lane(const Params& p, int e, Lane& L, bool 
     L.in_grid = valid && (f & F_IN_GRID); L.live = valid && (f & F_LIVE); L.active = valid && (f & F_ACTIVE);
     L.obs_m2 = valid && (f & F_OBS_M2);
     L.reward = 0.0;
+    L.ammo = valid ? am : 0;
 }
 
+template <bool AMMO = true>
 __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L, bool valid)
 {
     if (!valid) return;
@@ -638,6 +647,7 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
     p.health[k] = L.health;
     p.flags[k] = (uint8_t)((L.in_grid ? F_IN_GRID : 0) | (L.live ? F_LIVE : 0) | (L.active ? F_ACTIVE : 0) |
                            (L.obs_m2 ? F_OBS_M2 : 0));
+    if (AMMO) p.ammo[k] = L.ammo;
 }
 
 // LDS carve-up per wave (dynamic shared memory, 16-B aligned pieces)
@@ -1389,6 +1399,30 @@ __device__ __forceinline__ bool attack_precheck(const Params& p, const Smem& sm,
     return any;
 }
 
+// AttackActorBaseComponent.process_action's ammo filter (actor.py:343-351)
+// for AmmoAgent attacker a (uniform): more attacked entries than ammo keeps
+// np.random.choice(attacked, ammo, replace=False) = entries permutation(n)[:ammo]
+// in that order (n - 1 interval draws, also for ammo 0); then ammo -= the
+// kept count.  list: lane t holds entry t.
+__device__ __forceinline__ void ammo_filter(Rng& rng, Lane& L, int a, int& nlist, int& list)
+{
+    const int l = lane_id();
+    const int am = rl(L.ammo, a);
+    if (nlist > am) {
+        int perm = l;
+        for (int i = nlist - 1; i >= 1; i--) {
+            const int j = (int)rng.interval((uint32_t)i);
+            const int pi = rl(perm, i), pj = rl(perm, j);
+            if (l == i) perm = pj;
+            if (l == j) perm = pi;
+        }
+        const int kept = __shfl(list, l < am ? perm : 0);
+        list = l < am ? kept : -1;
+        nlist = am;
+    }
+    if (l == a) L.ammo = am - nlist;
+}
+
 // BinaryAttackActor.process_action for attacker a with k attacks.
 // Returns status (attempted); list (register of lane t) = attacked lanes in
 // list order; applies damage and updates the cell table for kills.
@@ -1488,6 +1522,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         const int lane_t = first_lane(tm);
         if (l == t) list = lane_t;
     }
+    if (!PLAIN && (akind & GW_K_AMMO)) ammo_filter(rng, L, a, nlist, list);
     // apply damage in list order (actor.py:353-358)
     const double strength = rld(L.strength, a);
     for (int t = 0; t < nlist; t++) {
@@ -1621,6 +1656,7 @@ __device__ __forceinline__ bool attack_selective(const Params& p, Smem& sm, Rng&
         }
         nlist += take;
     }
+    if (akind & GW_K_AMMO) ammo_filter(rng, L, a, nlist, list);
     // apply damage in list order (actor.py:353-358)
     const double strength = rld(L.strength, a);
     for (int t = 0; t < nlist; t++) {
@@ -2190,6 +2226,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         STAMP(15);
     }
     if (what == 3 && valid && !(L.kind & GW_K_HEALTH)) L.active = true;   // PrincipleAgent.active
+    // AmmoState.reset (state.py:644-656): no draw, any place in the state order
+    if (what == 3 && valid && (L.kind & GW_K_AMMO)) L.ammo = p.spec[l].init_ammo;
     return ok;
 }
 
@@ -2294,7 +2332,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     const int32_t steps_raw = p.steps[e];
     const uint32_t ad_raw = p.ad_in ? p.ad_in[e] : 0u;
     Lane L;
-    load_lane(p, e, L, valid);
+    load_lane<!PLAIN>(p, e, L, valid);
     // actions (lane = agent); attack == -1 marks "not in action_dict"
     const size_t EA = (size_t)p.E * A;
     const size_t act_row = ((size_t)e * A + (valid ? l : 0)) * p.act_dim;
@@ -2727,7 +2765,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         if (p.acting) p.acting[e] = acting_raw + acting_sum;
         if (p.ad_out) p.ad_out[e] = (uint8_t)prev_all;
     }
-    store_lane(p, e, L, valid);
+    store_lane<!PLAIN>(p, e, L, valid);
     store_rng(p, e, sm, rng, ctr);
     STAMP(6);
     STAMP_WAVE(61, false);
@@ -2759,6 +2797,12 @@ __device__ __forceinline__ void observe_absolute(const Params& p, const Smem& sm
         for (uint64_t it = blk; it; it &= it - 1) {
             const int b = first_lane(it);
             const int dr = rl(L.r, b) - ra, dc = rl(L.c, b) - ca;
+            if (dr >= -v && dr <= v && dc >= -v && dc <= v && shadow_hides(dr, dc, gr - ra, gc - ca))
+                h = true;
+        }
+        for (int q = 0; q < p.n_sblk; q++) {          // static blockers: always active
+            const int32_t sc = p.sblk[q];
+            const int dr = (sc >> 16) - ra, dc = (sc & 0xffff) - ca;
             if (dr >= -v && dr <= v && dc >= -v && dc <= v && shadow_hides(dr, dc, gr - ra, gc - ca))
                 h = true;
         }
@@ -3216,6 +3260,15 @@ struct gw_engine {
     int32_t n_ent;             // gw_config.n_agents (lanes + static entities)
 };
 
+// gw_set_launch_events arms the NEXT kernel launch of the handle's step /
+// reset kernels (part_launch / launch_pac consume and clear them).  Every
+// other entry point, and every early return, clears them on exit, so a
+// later unrelated launch never records them.
+struct EvClear {
+    gw_engine* g;
+    ~EvClear() { if (g) g->ev0 = g->ev1 = nullptr; }
+};
+
 // create_grid_and_mask (utils.py:46-115): the window cells of range R that a
 // blocker at offset (rd, cd) hides, as bits k = (r+R)(2R+1) + (c+R)
 // (shadow_hides, the reference's arithmetic in double).
@@ -3325,7 +3378,7 @@ static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 4; }
+int32_t gw_abi_version(void) { return 5; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
@@ -3520,6 +3573,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     HIPCHK(hipMemset(p.seq, 0, EA * sizeof(uint32_t)));
     HIPCHK(hipMemset(p.mt, 0, (size_t)n_envs * GW_MT_STRIDE * sizeof(uint32_t)));
     HIPCHK(hipMemset(p.steps, 0, (size_t)n_envs * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&p.ammo, EA * sizeof(int32_t)));
+    HIPCHK(hipMemset(p.ammo, 0, EA * sizeof(int32_t)));
     DevAgent hs[GW_MAX_LANES];
     for (int l = 0; l < A; l++) {
         const gw_agent_spec& s = cfg->agents[lanes[l]];
@@ -3531,6 +3586,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].init_health = s.initial_health;
         hs[l].init_orient = s.initial_orientation;
         hs[l].tgt_lane = -1; hs[l].tgt_pos = 0; hs[l].dtgt_lane = -1;
+        hs[l].init_ammo = (s.kind & GW_K_AMMO) ? s.initial_ammo : 0;
     }
     for (int l = 0; l < GW_MAX_LANES; l++) {
         g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
@@ -3662,7 +3718,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         }
         std::vector<int> sblock;
         for (int a : statics) if (cfg->agents[a].kind & GW_K_BLOCKING) sblock.push_back(a);
-        if (big && !sblock.empty()) {           // observe_big: the static blockers' cells
+        if (!sblock.empty()) {                  // observe_big / observe_absolute: the static blockers' cells
             std::vector<int32_t> sl;
             for (int a : sblock) sl.push_back((cfg->agents[a].init_row << 16) | cfg->agents[a].init_col);
             HIPCHK(hipMalloc(&g->d_sblk, sl.size() * 4));
@@ -3838,8 +3894,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     else if (!pac) HIPCHK(set_part_attrs(g->S, PK_STEP, PK_RESET, g->smem_step, g->smem_reset));
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
+    bool any_ammo = false;
+    for (int l = 0; l < A; l++) any_ammo |= (hs[l].kind & GW_K_AMMO) != 0;
     g->step_tb = GW_STEP_SPEC && !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
-                 !p.hetero_view;
+                 !p.hetero_view && !any_ammo;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));
     // MazeNavigation with the navigator and the target as its only lanes
     // (walls static), both at initial positions that never fail to place, no
@@ -3883,6 +3941,7 @@ gw_status gw_destroy(gw_handle g)
     if (!g) return GW_E_INVALID;
     (void)hipFree(g->base.pos); (void)hipFree(g->base.health); (void)hipFree(g->base.flags);
     (void)hipFree(g->base.seq); (void)hipFree(g->base.mt); (void)hipFree(g->base.steps);
+    (void)hipFree(g->base.ammo);
     (void)hipFree(g->d_spec); (void)hipFree(g->d_tmpl); (void)hipFree(g->d_free);
     (void)hipFree(g->d_static_bits); (void)hipFree(g->d_shadow); (void)hipFree(g->d_smask);
     (void)hipFree(g->base.racc); (void)hipFree(g->base.pbits); (void)hipFree(g->base.cyc);
@@ -3905,6 +3964,7 @@ int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
 
 gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     if (n == 0 || !lane_order) { g->base.act_order = nullptr; g->base.act_rank = nullptr; return GW_OK; }
     if (n != g->E * g->A) { set_err("action order: %d entries, expected E*A = %d", n, g->E * g->A); return GW_E_INVALID; }
@@ -3938,6 +3998,7 @@ gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
 
 gw_status gw_set_placement_order(gw_handle g, const int32_t* lane_order, int32_t n)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     if (n == 0 || !lane_order) {
         g->base.place_order = nullptr;
@@ -3976,6 +4037,7 @@ gw_status gw_lane_entities(gw_handle g, int32_t* out)
 
 gw_status gw_seed(gw_handle g, const uint32_t* seeds, void* stream)
 {
+    EvClear ec{g};
     if (!g || !seeds) return GW_E_INVALID;
     hipLaunchKernelGGL(seed_kernel, dim3((g->E + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        g->base.mt, seeds, g->E);
@@ -3986,6 +4048,7 @@ gw_status gw_seed(gw_handle g, const uint32_t* seeds, void* stream)
 gw_status gw_reset(gw_handle g, const uint8_t* mask, const uint8_t* all_done, int32_t horizon,
                    int32_t* obs, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !obs) return GW_E_INVALID;
     Params p = g->base;
     p.mask = mask; p.prev_all_done = all_done; p.horizon = horizon; p.obs = obs; p.err = err_flags;
@@ -3996,6 +4059,7 @@ gw_status gw_reset(gw_handle g, const uint8_t* mask, const uint8_t* all_done, in
 gw_status gw_step(gw_handle g, const int32_t* actions, int32_t* obs, double* reward,
                   uint8_t* done, uint8_t* all_done, uint64_t* acting, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
@@ -4011,6 +4075,7 @@ gw_status gw_step_autoreset(gw_handle g, const int32_t* actions, int32_t* obs, d
                             uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
                             uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
@@ -4027,6 +4092,7 @@ gw_status gw_step_autoreset_next(gw_handle g, const int32_t* actions, int32_t* o
                                  uint8_t* done, uint8_t* all_done, uint64_t* acting, int32_t horizon,
                                  uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !obs || !reward || !done || !all_done) return GW_E_INVALID;
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
@@ -4042,6 +4108,7 @@ gw_status gw_step_autoreset_next(gw_handle g, const int32_t* actions, int32_t* o
 gw_status gw_get_state(gw_handle g, int32_t* pos, double* health, uint8_t* flags, uint32_t* seq,
                        uint32_t* mt, int32_t* steps, void* stream)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
     const size_t EA = (size_t)g->E * g->A;
@@ -4061,6 +4128,7 @@ gw_status gw_get_state(gw_handle g, int32_t* pos, double* health, uint8_t* flags
 gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, const uint8_t* flags,
                        const uint32_t* seq, const uint32_t* mt, const int32_t* steps, void* stream)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
     const size_t EA = (size_t)g->E * g->A;
@@ -4082,6 +4150,22 @@ gw_status gw_set_state(gw_handle g, const int32_t* pos, const double* health, co
     return GW_OK;
 }
 
+gw_status gw_get_ammo(gw_handle g, int32_t* ammo, void* stream)
+{
+    EvClear ec{g};
+    if (!g || !ammo) return GW_E_INVALID;
+    HIPCHK(hipMemcpyAsync(ammo, g->base.ammo, (size_t)g->E * g->A * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return GW_OK;
+}
+
+gw_status gw_set_ammo(gw_handle g, const int32_t* ammo, void* stream)
+{
+    EvClear ec{g};
+    if (!g || !ammo) return GW_E_INVALID;
+    HIPCHK(hipMemcpyAsync(g->base.ammo, ammo, (size_t)g->E * g->A * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return GW_OK;
+}
+
 gw_status gw_obs_shape(gw_handle g, int32_t* rows, int32_t* cols)
 {
     if (!g || !rows || !cols) return GW_E_INVALID;
@@ -4095,6 +4179,7 @@ int32_t gw_num_passive(gw_handle g) { return g ? g->base.n_passive : 0; }
 gw_status gw_turn_reset(gw_handle g, const uint8_t* mask, int32_t* obs, uint8_t* returned,
                         int32_t* turn, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !obs || !returned || !turn) return GW_E_INVALID;
     if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
     Params p = g->base;
@@ -4111,6 +4196,7 @@ gw_status gw_turn_step(gw_handle g, const int32_t* actions, int32_t* obs, double
                        uint8_t* done, uint8_t* all_done, uint8_t* returned, int32_t* turn,
                        uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !obs || !reward || !done || !all_done || !returned || !turn) return GW_E_INVALID;
     if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
     Params p = g->base;
@@ -4126,6 +4212,7 @@ gw_status gw_turn_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, 
                           uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint8_t* returned,
                           int32_t* turn, uint64_t* acting, int32_t horizon, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || n_steps <= 0 || !actions || !obs || !reward || !done || !all_done || !returned || !turn)
         return GW_E_INVALID;
     if (!g->pacman) { set_err("turn-based protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
@@ -4140,6 +4227,7 @@ gw_status gw_turn_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, 
 
 gw_status gw_sim_reset(gw_handle g, const uint8_t* mask, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     if (!g->pacman) { set_err("simulation-only protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
     Params p = g->base;
@@ -4151,6 +4239,7 @@ gw_status gw_sim_reset(gw_handle g, const uint8_t* mask, uint32_t* err_flags, vo
 gw_status gw_sim_step(gw_handle g, const int32_t* actions, double* reward, uint8_t* done,
                       uint8_t* all_done, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !reward || !done || !all_done) return GW_E_INVALID;
     if (!g->pacman) { set_err("simulation-only protocol: Pacman program only"); return GW_E_UNSUPPORTED; }
     Params p = g->base;
@@ -4162,6 +4251,7 @@ gw_status gw_sim_step(gw_handle g, const int32_t* actions, double* reward, uint8
 
 gw_status gw_observe(gw_handle g, int32_t lane, int32_t* obs, void* stream)
 {
+    EvClear ec{g};
     if (!g || !obs || lane < 0 || lane >= g->A) return GW_E_INVALID;
     if (!g->pacman) { set_err("on-demand observation: Pacman program only"); return GW_E_UNSUPPORTED; }
     Params p = g->base;
@@ -4173,6 +4263,7 @@ gw_status gw_observe(gw_handle g, int32_t lane, int32_t* obs, void* stream)
 gw_status gw_get_aux_state(gw_handle g, double* racc, uint32_t* passive_bits, int32_t* turn_pos,
                            void* stream)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
     const size_t EA = (size_t)g->E * g->A;
@@ -4186,6 +4277,7 @@ gw_status gw_get_aux_state(gw_handle g, double* racc, uint32_t* passive_bits, in
 gw_status gw_set_aux_state(gw_handle g, const double* racc, const uint32_t* passive_bits,
                            const int32_t* turn_pos, void* stream)
 {
+    EvClear ec{g};
     if (!g) return GW_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
     const size_t EA = (size_t)g->E * g->A;
@@ -4215,6 +4307,7 @@ gw_status gw_debug_set_stamps(gw_handle g, uint64_t* stamps)
 gw_status gw_random_actions(gw_handle g, uint64_t key, uint32_t step, uint32_t env_offset,
                             int32_t* actions, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions) return GW_E_INVALID;
     const dim3 grid = g->A <= WAVE ? dim3((g->E + 15) / 16) : dim3((unsigned)(((size_t)g->E * g->A + 255) / 256));
     hipLaunchKernelGGL(random_actions_kernel, grid, dim3(g->A <= WAVE ? 16 * WAVE : 256), 0,
@@ -4229,10 +4322,14 @@ gw_status gw_rollout_step(gw_handle g, uint64_t key, uint32_t step, uint32_t env
                           uint8_t* all_done, uint64_t* acting, int32_t horizon, int32_t autoreset,
                           uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || !actions || !obs || !reward || !done || !all_done || autoreset < 0 || autoreset > 2)
         return GW_E_INVALID;
+    // the armed launch events belong to the step, not to the action kernel
+    const hipEvent_t ev0 = g->ev0, ev1 = g->ev1;
     const gw_status s = gw_random_actions(g, key, step, env_offset, actions, stream);
     if (s != GW_OK) return s;
+    g->ev0 = ev0; g->ev1 = ev1;
     Params p = g->base;
     p.actions = actions; p.obs = obs; p.reward = reward; p.done = done; p.all_done = all_done;
     p.acting = acting; p.autoreset = autoreset; p.horizon = horizon; p.err = err_flags;
@@ -4263,6 +4360,7 @@ static gw_status maze_launch(gw_engine* g, int mode, const int32_t* args, const 
 
 gw_status gw_generate_maze(gw_handle g, const int32_t* start, int8_t* maze, void* stream)
 {
+    EvClear ec{g};
     if (!g || !maze) return GW_E_INVALID;
     if (g->pacman) { set_err("generate_maze: not on a Pacman handle"); return GW_E_UNSUPPORTED; }
     return maze_launch(g, 0, nullptr, start, maze, nullptr, nullptr, (hipStream_t)stream);
@@ -4271,6 +4369,7 @@ gw_status gw_generate_maze(gw_handle g, const int32_t* start, int8_t* maze, void
 gw_status gw_component(gw_handle g, int32_t op, int32_t lane, const int32_t* args, int32_t* result,
                        int32_t* obs, uint32_t* err_flags, void* stream)
 {
+    EvClear ec{g};
     if (!g || op < GW_OP_POSITION_RESET || op > GW_OP_OBSERVE_ABS) return GW_E_INVALID;
     if (g->pacman) {
         set_err("component operations run on the one-wave and workgroup engines (not the Pacman kernel)");
@@ -4304,6 +4403,7 @@ gw_status gw_rollout(gw_handle g, int32_t n_steps, const int32_t* actions, int32
                      int32_t horizon, int32_t autoreset, int32_t skip_done_obs, uint32_t* err_flags,
                      void* stream)
 {
+    EvClear ec{g};
     if (!g || n_steps <= 0 || !actions || !obs || !reward || !done || !all_done ||
         autoreset < 1 || autoreset > 2)
         return GW_E_INVALID;

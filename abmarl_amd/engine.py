@@ -558,6 +558,19 @@ class GridWorldEngine:
                                                          'steps')], _stream()), 'gw_get_state')
         return st
 
+    def get_ammo(self):
+        """AmmoAgent.ammo of every lane: int32[E][A] (0 for other lanes)."""
+        out = torch.zeros((self.E, self.A), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_get_ammo(self.h, _ptr(out), _stream()), 'gw_get_ammo')
+        return out
+
+    def set_ammo(self, ammo):
+        a = torch.as_tensor(ammo, dtype=torch.int32, device=self.device).reshape(self.E, self.A).contiguous()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_set_ammo(self.h, _ptr(a), _stream()), 'gw_set_ammo')
+            torch.cuda.current_stream().synchronize()
+
     def set_state(self, pos=None, health=None, flags=None, seq=None, mt=None, steps=None):
         with torch.cuda.device(self.device):
             _native.check(self.L.gw_set_state(self.h, _ptr(pos), _ptr(health), _ptr(flags),

@@ -202,6 +202,34 @@ class AttackingAgent(ActingAgent, GridWorldAgent):
             self.attack_strength is not None and self.attack_accuracy is not None
 
 
+class AmmoAgent(GridWorldAgent):
+    """agent.py:291-322: a limited number of attacks; AmmoState.reset gives
+    it initial_ammo, every attack spends what it lands (actor.py:343-351)."""
+
+    def __init__(self, initial_ammo=None, **kwargs):
+        super().__init__(**kwargs)
+        self.initial_ammo = initial_ammo
+
+    @property
+    def ammo(self):
+        return self._ammo
+
+    @ammo.setter
+    def ammo(self, value):
+        assert type(value) is int, "Ammo must be an integer."
+        self._ammo = 0 if value < 0 else value
+        host_version.bump()
+
+    @property
+    def initial_ammo(self):
+        return self._initial_ammo
+
+    @initial_ammo.setter
+    def initial_ammo(self, value):
+        assert type(value) is int, "Initial ammo must be a an integer."
+        self._initial_ammo = value
+
+
 class OrientationAgent(GridWorldAgent):
     """agent.py:342-373: orientation 1 left, 2 down, 3 right, 4 up;
     initial_orientation None means random at reset (OrientationState)."""

@@ -37,6 +37,33 @@ class GridWorldSimulation(AgentBasedSimulation, ABC):
         return cls._build_sim(rows, cols, **kwargs)
 
     @classmethod
+    def build_sim_from_grid(cls, grid, extra_agents=None, **kwargs):
+        """The agents of a Grid's cells, plus extra agents (base.py:61-96).
+
+        An agent found in the grid takes the place of an extra agent with the
+        same id (the extra_agents dict is updated in place, as the
+        reference's is); every agent in a cell must have that cell as its
+        initial position.  The new simulation gets a fresh, empty Grid of the
+        same size (placement happens at reset)."""
+        assert type(grid) is Grid, "Grid object required."
+        if extra_agents is not None:
+            assert type(extra_agents) is dict, "Extra agents must be a dictionary."
+            agents = extra_agents
+        else:
+            agents = {}
+        for r in range(grid.rows):
+            for c in range(grid.cols):
+                cell = grid[r, c]
+                if cell is None:
+                    continue
+                agents.update(cell)
+                for agent in cell.values():
+                    np.testing.assert_array_equal(
+                        agent.initial_position, np.array([r, c]),
+                        err_msg="The initial position of the agent must match its position in the grid.")
+        return cls._build_sim(grid.rows, grid.cols, agents=agents, **kwargs)
+
+    @classmethod
     def build_sim_from_array(cls, array, object_registry, extra_agents=None, **kwargs):
         """Agents from a character array, in row-major order (base.py:98-141)."""
         assert type(array) is np.ndarray, "The array must be a numpy array."

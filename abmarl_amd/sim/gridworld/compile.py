@@ -14,9 +14,11 @@ lowered here, once, to constant tables:
 from abmarl_amd import _abi
 from abmarl_amd.sim.agent_based_simulation import ObservingAgent, ActingAgent
 from abmarl_amd.sim.gridworld.agent import (
-    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, OrientationAgent)
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, OrientationAgent,
+    AmmoAgent)
 from abmarl_amd.sim.gridworld.components import (
-    PositionState, HealthState, OrientationState, BinaryAttackActor, SelectiveAttackActor,
+    PositionState, HealthState, OrientationState, AmmoState, _TargetPlacementState,
+    BinaryAttackActor, SelectiveAttackActor,
     PositionCenteredEncodingObserver, AbsoluteEncodingObserver, ActiveDone, OneTeamRemainingDone,
     TargetAgentDone, TargetDestroyedDone, MoveActor, DriftMoveActor)
 
@@ -47,6 +49,8 @@ def agent_spec(agent, program_type=None, food_type=None):
         kind |= _abi.GW_K_HEALTH
     if agent.blocking:
         kind |= _abi.GW_K_BLOCKING
+    if isinstance(agent, AmmoAgent):
+        kind |= _abi.GW_K_AMMO
     s = _abi.AgentSpec()
     s.encoding = agent.encoding
     s.kind = kind
@@ -63,6 +67,7 @@ def agent_spec(agent, program_type=None, food_type=None):
     ih = getattr(agent, 'initial_health', None)
     s.initial_health = -1.0 if ih is None else float(ih)
     s.initial_orientation = int(getattr(agent, 'initial_orientation', None) or 0)
+    s.initial_ammo = int(agent.initial_ammo) if isinstance(agent, AmmoAgent) else 0
     return s
 
 
@@ -85,12 +90,23 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
     if sim.grid.rows * sim.grid.cols > _abi.GW_MAX_CELLS:
         raise UnsupportedConfig(f"grid larger than {_abi.GW_MAX_CELLS} cells")
 
+    for s in states:
+        if isinstance(s, _TargetPlacementState):
+            raise UnsupportedConfig(f"{type(s).__name__} runs through the component API "
+                                    "(a simulation without an engine program)")
+        if not isinstance(s, (PositionState, HealthState, OrientationState, AmmoState)):
+            raise UnsupportedConfig(f"{type(s).__name__} has no HIP implementation")
     pos_states = [s for s in states if isinstance(s, PositionState)]
     health_states = [s for s in states if isinstance(s, HealthState)]
     if len(pos_states) != 1:
         raise UnsupportedConfig("exactly one PositionState is required")
     if any(isinstance(a, HealthAgent) for a in agents) and not health_states:
         raise UnsupportedConfig("HealthAgents require a HealthState")
+    if any(isinstance(a, AmmoAgent) and isinstance(a, AttackingAgent) for a in agents) and \
+            not any(isinstance(s, AmmoState) for s in states):
+        # without AmmoState.reset the agent has no ammo: the reference raises
+        # AttributeError at its first attack (actor.py:346)
+        raise UnsupportedConfig("attacking AmmoAgents require an AmmoState")
 
     obs_range = 0
     observe_self = True

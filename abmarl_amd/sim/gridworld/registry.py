@@ -1,7 +1,12 @@
 """Component registry (reference: abmarl/sim/gridworld/registry.py:14-77).
 
-Only components the engine can execute are registered; ``register`` of any
-other subclass raises, because the fused step cannot run arbitrary Python.
+``register`` accepts any subclass of a component base, as the reference's
+does.  A user-written component runs as the user's own Python on the host
+Grid / agents (a simulation without an engine program drives its components
+one call at a time; the built-in ones there are device operations, and the
+component runtime re-uploads whatever the user's code changed before the next
+one).  The fused engine programs (TeamBattleSim, ...) compile only the
+built-in components and refuse others at construction.
 """
 from abmarl_amd.sim.gridworld.components import (
     ActorBaseComponent, MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor,
@@ -9,7 +14,7 @@ from abmarl_amd.sim.gridworld.components import (
     TargetDestroyedDone,
     ObserverBaseComponent, PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
     StateBaseComponent, PositionState, MazePlacementState, TargetBarriersFreePlacementState,
-    HealthState, OrientationState,
+    HealthState, OrientationState, AmmoState,
 )
 
 _subclass_check_mapping = {
@@ -24,7 +29,7 @@ _registered_components = {
     'done': {ActiveDone, OneTeamRemainingDone, TargetAgentDone, TargetDestroyedDone},
     'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
     'state': {PositionState, MazePlacementState, TargetBarriersFreePlacementState, HealthState,
-              OrientationState},
+              AmmoState, OrientationState},
 }
 
 registry = {
@@ -33,14 +38,10 @@ registry = {
 
 
 def register(component):
-    """Register an engine-executable component under its type and class name."""
+    """Register a component by its type (actor, done, observer or state) and
+    class name (registry.py:58-77); anything else raises TypeError."""
     for kind, base in _subclass_check_mapping.items():
-        if issubclass(component, base):
-            if not any(issubclass(component, c) for c in _registered_components[kind]):
-                raise TypeError(
-                    f"{component.__name__} has no HIP implementation; only subclasses of "
-                    f"{sorted(c.__name__ for c in _registered_components[kind])} can run on the "
-                    "engine.")
+        if isinstance(component, type) and issubclass(component, base):
             _registered_components[kind].add(component)
             registry[kind][component.__name__] = component
             return

@@ -16,7 +16,7 @@ import torch
 
 from abmarl_amd import _abi
 from abmarl_amd.engine import GridWorldEngine
-from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent, OrientationAgent
+from abmarl_amd.sim.gridworld.agent import HealthAgent, GridObservingAgent, OrientationAgent, AmmoAgent
 
 
 class DictRuntime:
@@ -49,6 +49,7 @@ class DictRuntime:
         self.sides = [2 * a.view_range + 1 if isinstance(a, GridObservingAgent) else 0
                       for a in sim.agents.values()]
         self.lazy = compiled.cfg.sim_kind == _abi.GW_SIM_PACMAN
+        self.has_ammo = any(isinstance(a, AmmoAgent) for a in sim.agents.values())
         # PositionState(randomize_placement_order=True): the component's own
         # agents dict, reshuffled in place at every reset (state.py:97-101)
         self.place_items = list(range(len(self.ids))) if compiled.randomize_placement_order else None
@@ -75,6 +76,8 @@ class DictRuntime:
         st = self.eng.get_state()
         if self.lazy:
             aux = self.eng.get_aux_state()
+        if self.has_ammo:
+            st['ammo'] = self.eng.get_ammo()
         torch.cuda.synchronize(self.dev)
         host = {k: v.cpu().numpy() for k, v in st.items()}
         pbits = aux['passive'].cpu().numpy().view(np.uint32)[0] if self.lazy else None
@@ -102,6 +105,8 @@ class DictRuntime:
             agent.position = host['pos'][0, k].astype(int)
             if isinstance(agent, HealthAgent):
                 agent._health = float(host['health'][0, k])
+            if isinstance(agent, AmmoAgent):
+                agent._ammo = int(host['ammo'][0, k])
             agent._active = bool(flags[k] & _abi.FLAG_ACTIVE)
 
     # ------------------------------------------------- lazy (Pacman) protocol

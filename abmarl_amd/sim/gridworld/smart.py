@@ -84,7 +84,11 @@ class SmartGridWorldSimulation(GridWorldSimulation, ABC):
         """This simulation as an engine configuration (_abi.CompiledConfig)."""
         assert self._engine_program is not None, \
             f"{type(self).__name__} has no engine step program"
-        return compile_sim(self, self._engine_program, self._states, self._observers,
+        # the states of the sets, and those a subclass holds as attributes
+        # (e.g. an AmmoState added to an example program)
+        states = list(self._states) + [v for v in vars(self).values()
+                                       if isinstance(v, StateBaseComponent) and v not in self._states]
+        return compile_sim(self, self._engine_program, states, self._observers,
                            self._dones, self._actors(), self.state_order,
                            **self._program_extras())
 

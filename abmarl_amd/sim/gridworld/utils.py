@@ -1,14 +1,79 @@
-"""generate_maze (reference: abmarl/sim/gridworld/utils.py:120-212) on the
-device: Prim's algorithm drawing from the global np.random stream, with the
-frontier in CPython's list(set(...)) order exactly as the reference
-(gw_generate_maze, csrc/gw_maze.inc).  The numpy RNG state is handed to the
-engine before the call and taken back after it, so the caller's stream
-advances by exactly the reference's draws.
+"""GridWorld utilities (reference: abmarl/sim/gridworld/utils.py).
+
+generate_maze (utils.py:120-212) runs on the device: Prim's algorithm drawing
+from the global np.random stream, with the frontier in CPython's
+list(set(...)) order exactly as the reference (gw_generate_maze,
+csrc/gw_maze.inc).  The numpy RNG state is handed to the engine before the
+call and taken back after it, so the caller's stream advances by exactly the
+reference's draws.
+
+create_grid_and_mask (utils.py:5-117) is the host form for user-written
+components (registry.register): the built-in components evaluate the same
+masks on the device (shadow LUTs and shadow_hides in csrc/gw_engine.hip).
 """
 import numpy as np
 import torch
 
 from abmarl_amd import _abi
+
+
+def shadow_hidden(rd, cd, r, c):
+    """Which window offsets (r, c) (integer arrays) a blocker at offset
+    (rd, cd) hides: the cells strictly between the two rays from the
+    observer's center through the blocker cell's corners, on the far side of
+    the blocker (utils.py:46-115, the eight cases in the reference's float64
+    arithmetic); never the blocker's own cell.  The device's shadow_hides is
+    the same function."""
+    r = np.asarray(r)
+    c = np.asarray(c)
+    if rd == 0 and cd == 0:
+        return np.zeros(np.broadcast(r, c).shape, dtype=bool)
+    rd_f, cd_f = float(rd), float(cd)
+    if cd == 0:                                     # below / above: rays in c
+        far = r >= rd if rd > 0 else r <= rd
+        dd = -0.5 if rd > 0 else 0.5
+        left = (cd_f - 0.5) / (rd_f + dd) * r
+        right = (cd_f + 0.5) / (rd_f + dd) * r
+        hide = far & (left < c) & (c < right)
+    else:                                           # rays in r
+        far = c >= cd if cd > 0 else c <= cd
+        if rd > 0:
+            far = far & (r >= rd)
+        elif rd < 0:
+            far = far & (r <= rd)
+        if rd == 0:
+            lo_d = up_d = -0.5 if cd > 0 else 0.5   # right / left
+        elif (rd > 0) == (cd > 0):
+            lo_d, up_d = 0.5, -0.5                  # below-right / above-left
+        else:
+            lo_d, up_d = -0.5, 0.5                  # below-left / above-right
+        lo = (rd_f - 0.5) / (cd_f + lo_d) * c
+        up = (rd_f + 0.5) / (cd_f + up_d) * c
+        hide = far & (lo < r) & (r < up)
+    return hide & ~((r == rd) & (c == cd))
+
+
+def create_grid_and_mask(agent, grid, mask_range, agents):
+    """The (2R+1)^2 local grid around the agent (grid cells, None off the
+    grid) and its visibility mask (1 visible, 0 hidden behind an active
+    blocking agent), as utils.py:5-117 returns them."""
+    d = 2 * mask_range + 1
+    local_grid = np.empty((d, d), dtype=object)
+    r, c = agent.position
+    r_lower, r_upper = max(0, r - mask_range), min(grid.rows - 1, r + mask_range) + 1
+    c_lower, c_upper = max(0, c - mask_range), min(grid.cols - 1, c + mask_range) + 1
+    local_grid[(r_lower + mask_range - r):(r_upper + mask_range - r),
+               (c_lower + mask_range - c):(c_upper + mask_range - c)] = \
+        grid[r_lower:r_upper, c_lower:c_upper]
+    mask = np.ones((d, d))
+    off = np.arange(-mask_range, mask_range + 1)
+    rr, cc = np.meshgrid(off, off, indexing='ij')
+    for other in agents.values():
+        if other.active and other.blocking:
+            rd, cd = other.position - agent.position
+            if -mask_range <= rd <= mask_range and -mask_range <= cd <= mask_range:
+                mask[shadow_hidden(int(rd), int(cd), rr, cc)] = 0
+    return local_grid, mask
 
 _engines = {}
 

@@ -135,6 +135,12 @@ class Dict(Space):
     def __setitem__(self, k, v):
         self.spaces[k] = v
 
+    def __iter__(self):
+        return iter(self.spaces)
+
+    def __len__(self):
+        return len(self.spaces)
+
     def keys(self):
         return self.spaces.keys()
 

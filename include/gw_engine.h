@@ -122,6 +122,9 @@ typedef int32_t gw_status;
 #define GW_K_LANE         0x400u /* never a static entity: the caller may read or edit
                                     it (the component runtime keeps blocking entities
                                     as lanes: the absolute observer's masks take lanes) */
+#define GW_K_AMMO         0x800u /* AmmoAgent                 gridworld/agent.py:291-322: a
+                                    limited number of attacks (AttackActorBaseComponent.
+                                    process_action's ammo filter, actor.py:343-351) */
 #define GW_K_BLOCKING      0x40u /* GridWorldAgent.blocking   gridworld/agent.py:66-75;
                                     active blocking entities mask cells from
                                     observers and attackers (utils.py:5-117) */
@@ -174,6 +177,8 @@ typedef struct gw_agent_spec {
     int32_t  initial_orientation;  /* OrientationAgent: 1..4, 0 = None (randint(1, 5)) */
     int32_t  done_target;          /* TargetAgentDone.target_mapping[this] (entity index), -1 */
     int32_t  destroy_target;       /* TargetDestroyedDone.target_mapping[this], -1            */
+    int32_t  initial_ammo;         /* AmmoAgent.initial_ammo (GW_K_AMMO): the ammo every reset
+                                      gives it (AmmoState.reset, state.py:644-656)           */
 } gw_agent_spec;
 
 typedef struct gw_config {
@@ -318,6 +323,17 @@ gw_status gw_get_state(gw_handle h, int32_t* pos, double* health, uint8_t* flags
 gw_status gw_set_state(gw_handle h, const int32_t* pos, const double* health,
                        const uint8_t* flags, const uint32_t* seq, const uint32_t* mt,
                        const int32_t* steps, void* stream);
+
+/* AmmoAgent.ammo of every lane (GW_K_AMMO lanes; 0 for the others), the
+   state beside gw_get_state: device int32[E][A].  Every reset of an env
+   (gw_reset, the auto-reset calls, gw_sim_reset) sets its ammo lanes to
+   initial_ammo (AmmoState.reset, state.py:644-656: no draw, so its place
+   in the state order changes nothing); every attack of an ammo lane with
+   more attacked entries than ammo keeps np.random.choice(attacked, ammo,
+   replace=False) of them (= permutation(n)[:ammo] draws) and subtracts the
+   kept count (actor.py:343-351).                                          */
+gw_status gw_get_ammo(gw_handle h, int32_t* ammo, void* stream);
+gw_status gw_set_ammo(gw_handle h, const int32_t* ammo, void* stream);
 
 /* Philox-4x32-10 random policy (uniform over MoveActor Box(-r,r,(2,)) and
    BinaryAttackActor Discrete(k+1)): actions for every entity of every env,

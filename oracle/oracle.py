@@ -51,6 +51,7 @@ def lib():
         L.gwo_get_err.argtypes = [vp, vp]
         L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
+        L.gwo_get_ammo.argtypes = [vp, vp]
         L.gwo_mt_probe.argtypes = [C.c_uint32, C.c_int32, C.c_uint32, C.c_int32, vp]
         L.gwo_turn_reset.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_turn_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -170,6 +171,12 @@ class Oracle:
         steps = np.zeros(E, np.int32)
         self.L.gwo_get_state(self.h, _p(pos), _p(health), _p(flags), _p(mt), _p(steps))
         return dict(pos=pos, health=health, flags=flags, mt=mt, steps=steps)
+
+    def ammo(self):
+        """AmmoAgent.ammo of every entity, int32[E][A]."""
+        out = np.zeros((self.E, self.A), np.int32)
+        self.L.gwo_get_ammo(self.h, _p(out))
+        return out
 
     def cells(self, env):
         out = np.zeros((self.cc.rows * self.cc.cols, self.A), np.int32)

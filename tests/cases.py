@@ -7,17 +7,40 @@ import numpy as np
 from abmarl_amd.examples import (TeamBattleSim, MazeNavigationAgent, MazeNavigationSim,
                                  ReachTheTargetSim, RunningAgent, TargetAgent, BarrierAgent)
 from abmarl_amd.sim.gridworld.agent import (
-    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent)
+    GridWorldAgent, GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, AmmoAgent)
+from abmarl_amd.sim.gridworld.components import AmmoState
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
                 'tb_destroy', 'tb_chase', 'tb_views', 'maze_file', 'maze_16', 'rtt_7', 'rtt_7_views',
                 'rtt_16', 'rtt_double', 'rtt_64', 'traffic_ex', 'traffic_9', 'tb_128', 'tb_100',
-                'rtt_16_example']
+                'rtt_16_example', 'tb_ammo', 'tb_ammo_multi', 'tb_ammo_stacked', 'rtt_ammo']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
     pass
+
+
+class AmmoFighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, AmmoAgent):
+    pass
+
+
+class AmmoTarget(TargetAgent, AmmoAgent):
+    """ReachTheTarget's target as an AmmoAgent (user-level class, as the
+    rtt_ammo fixture's generator defines it)."""
+
+
+class AmmoReachTheTargetSim(ReachTheTargetSim):
+    """The example program with an AmmoState beside its own states (a user's
+    subclass; the program compiles the extra state)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.ammo_state = AmmoState(**kwargs)
+
+    def reset(self, **kwargs):
+        super().reset(**kwargs)
+        self.ammo_state.reset(**kwargs)
 
 
 def load_golden(name):
@@ -54,7 +77,11 @@ def build_rtt(c, sim_cls=None):
     kw = dict(c['target'])
     if c.get('corners') or c.get('target_center'):
         kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
-    agents['target'] = TargetAgent(**kw)
+    if 'target_ammo' in c:
+        agents['target'] = AmmoTarget(initial_ammo=c['target_ammo'], **kw)
+        sim_cls = sim_cls or AmmoReachTheTargetSim
+    else:
+        agents['target'] = TargetAgent(**kw)
     ov = {int(k): set(v) for k, v in c['overlapping'].items()} if 'overlapping' in c \
         else {2: {3}, 3: {1, 2, 3}}
     return (sim_cls or ReachTheTargetSim).build_sim(R, C, agents=agents, overlapping=ov, attack_mapping={2: {3}})
@@ -111,14 +138,18 @@ def build_sim(c, sim_cls=None):
             kw['initial_health'] = c['initial_health'][str(i)]
         if i in c.get('blocking', []):
             kw['blocking'] = True
-        agents[kw['id']] = Fighter(**kw)
+        if c.get('ammo'):
+            kw['initial_ammo'] = c['ammo'][i % len(c['ammo'])]
+            agents[kw['id']] = AmmoFighter(**kw)
+        else:
+            agents[kw['id']] = Fighter(**kw)
     kwargs = dict(
         overlapping={int(k): set(v) for k, v in c['overlap'].items()},
         attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
         stacked_attacks=c['stacked_attacks'], observe_self=c['observe_self'],
         no_overlap_at_reset=c['no_overlap_at_reset'],
         randomize_placement_order=c.get('randomize_placement_order', False),
-        states={'PositionState', 'HealthState'},
+        states={'PositionState', 'HealthState'} | ({'AmmoState'} if c.get('ammo') else set()),
         observers={'PositionCenteredEncodingObserver'},
         dones=set(c.get('dones', ['OneTeamRemainingDone'])), state_order=c['state_order'])
     if 'target_mapping' in c:

@@ -90,6 +90,12 @@ def install():
         def __setitem__(self, k, v):
             self.spaces[k] = v
 
+        def __iter__(self):
+            return iter(self.spaces)
+
+        def __len__(self):
+            return len(self.spaces)
+
         def items(self):
             return self.spaces.items()
 

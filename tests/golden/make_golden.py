@@ -167,6 +167,37 @@ CASES = [
     dict(name='traffic_shuffle_act', kind='traffic', n_envs=4, n_steps=150, horizon=60, seed_base=63,
          randomize_action_input=True,
          grid=['G_WWWWW_R', 'G_______R', 'r___W___g', 'G_______R', 'G_WWWWW_R'], targets='team'),
+    # AmmoAgent fighters (agent.py:291-322) + AmmoState (state.py:644-656):
+    # up to 3 attacks a step against 1..5 rounds of ammo, so the ammo filter
+    # (actor.py:343-351) keeps choice(attacked, ammo, replace=False) of the
+    # attacked list, and attacks at 0 ammo still draw the permutation
+    dict(name='tb_ammo', rows=7, cols=7, n_agents=14, n_teams=2, n_envs=4, n_steps=140, horizon=45,
+         seed_base=201, ammo=[1, 3, 2], overlap={1: [1, 2], 2: [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=2)),
+    # several attacks a step (simultaneous_attacks 3, stacked or not), so the
+    # ammo filter draws its permutation over longer attacked lists.  The
+    # reference's TeamBattleSim.step tests `not attacked_agents`
+    # (team_battle_example.py:41), which raises ValueError on the numpy array
+    # _subset_attackables returns for two or more picks; these fixtures run
+    # the example with that test as `len(attacked_agents) == 0` (len_fix),
+    # the program's meaning, everything else the reference's own code
+    dict(name='tb_ammo_multi', rows=7, cols=7, n_agents=14, n_teams=2, n_envs=4, n_steps=140,
+         horizon=45, seed_base=207, ammo=[1, 3, 5, 2], attack_max=3, len_fix=True,
+         overlap={1: [1, 2], 2: [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=2, simultaneous_attacks=3)),
+    dict(name='tb_ammo_stacked', rows=6, cols=6, n_agents=10, n_teams=2, n_envs=4, n_steps=120,
+         horizon=40, seed_base=203, ammo=[2, 4], attack_max=2, stacked_attacks=True, len_fix=True,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=1,
+                    view_range=2, simultaneous_attacks=2)),
+    # ReachTheTarget whose target is an AmmoAgent (SelectiveAttackActor: two
+    # attacks per cell of its window) and an AmmoState beside the example's states
+    dict(name='rtt_ammo', kind='rtt', rows=9, cols=9, n_barriers=8, n_runners=20, n_envs=4,
+         n_steps=120, horizon=40, seed_base=205, target_ammo=6,
+         runner=dict(move_range=1, view_range=2, initial_health=1),
+         target=dict(view_range=2, attack_range=1, attack_strength=1, attack_accuracy=0.9,
+                     simultaneous_attacks=2)),
 ]
 
 DEFAULT_AGENT = dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
@@ -261,7 +292,7 @@ def make_actions(c, A, managers=None):
     mr = c['agent']['move_range']
     act = np.zeros((T, E, A, 3), dtype=np.int8)
     act[..., 0:2] = rng.randint(-mr, mr + 1, size=(T, E, A, 2))
-    act[..., 2] = rng.randint(0, 2, size=(T, E, A))
+    act[..., 2] = rng.randint(0, c.get('attack_max', 1) + 1, size=(T, E, A))
     return act
 
 
@@ -295,9 +326,29 @@ def build_reference_rtt(c):
     kw = dict(c['target'])
     if c.get('corners') or c.get('target_center'):
         kw['initial_position'] = np.array([R // 2, C // 2], dtype=int)
-    agents['target'] = TargetAgent(**kw)
-    sim = ReachTheTargetSim.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
-                                      attack_mapping={2: {3}})
+    sim_cls = ReachTheTargetSim
+    if 'target_ammo' in c:
+        from abmarl.sim.gridworld.agent import AmmoAgent
+        from abmarl.sim.gridworld.state import AmmoState
+
+        class AmmoTarget(TargetAgent, AmmoAgent):
+            pass
+
+        class AmmoReachTheTargetSim(ReachTheTargetSim):
+            def __init__(self, **kwargs):
+                super().__init__(**kwargs)
+                self.ammo_state = AmmoState(**kwargs)
+
+            def reset(self, **kwargs):
+                super().reset(**kwargs)
+                self.ammo_state.reset(**kwargs)
+
+        agents['target'] = AmmoTarget(initial_ammo=c['target_ammo'], **kw)
+        sim_cls = AmmoReachTheTargetSim
+    else:
+        agents['target'] = TargetAgent(**kw)
+    sim = sim_cls.build_sim(R, C, agents=agents, overlapping={2: {3}, 3: {1, 2, 3}},
+                            attack_mapping={2: {3}})
     return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
@@ -335,6 +386,35 @@ def build_reference_traffic(c):
     return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
+def len_fixed_team_battle(TeamBattleSim):
+    """team_battle_example.py:33-59 with its failed-attack test written as
+    len(attacked_agents) == 0 (the example's `not attacked_agents` raises
+    ValueError on a numpy array of two or more agents); the step is otherwise
+    the example's, statement for statement."""
+    class LenFixedTeamBattleSim(TeamBattleSim):
+        def step(self, action_dict, **kwargs):
+            for agent_id, action in action_dict.items():
+                attacking_agent = self.agents[agent_id]
+                if attacking_agent.active:
+                    status, attacked = self.attack_actor.process_action(attacking_agent, action, **kwargs)
+                    if status:
+                        if len(attacked) == 0:
+                            self.rewards[attacking_agent.id] -= 0.1
+                        else:
+                            for attacked_agent in attacked:
+                                if not attacked_agent.active:
+                                    self.rewards[attacked_agent.id] -= 1
+                                    self.rewards[attacking_agent.id] += 1
+            for agent_id, action in action_dict.items():
+                agent = self.agents[agent_id]
+                if agent.active:
+                    if not self.move_actor.process_action(agent, action, **kwargs):
+                        self.rewards[agent.id] -= 0.1
+            for agent_id in action_dict:
+                self.rewards[agent_id] -= 0.01
+    return LenFixedTeamBattleSim
+
+
 def build_reference_env(c):
     if c['kind'] == 'maze':
         return build_reference_maze(c)
@@ -346,10 +426,14 @@ def build_reference_env(c):
     from abmarl.sim.gridworld.agent import GridWorldAgent
     from abmarl.sim.gridworld.agent import GridObservingAgent, MovingAgent, AttackingAgent, \
         HealthAgent
-    from abmarl.sim.gridworld.state import PositionState, HealthState
+    from abmarl.sim.gridworld.agent import AmmoAgent
+    from abmarl.sim.gridworld.state import PositionState, HealthState, AmmoState
     from abmarl.managers import AllStepManager
 
     class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
+        pass
+
+    class AmmoFighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent, AmmoAgent):
         pass
 
     agents = {}
@@ -363,7 +447,11 @@ def build_reference_env(c):
             kw['initial_health'] = c['initial_health'][str(i)]
         if i in c['blocking']:
             kw['blocking'] = True
-        agents[kw['id']] = Fighter(**kw)
+        if c.get('ammo'):
+            kw['initial_ammo'] = c['ammo'][i % len(c['ammo'])]
+            agents[kw['id']] = AmmoFighter(**kw)
+        else:
+            agents[kw['id']] = Fighter(**kw)
     kwargs = dict(
         overlapping={int(k): set(v) for k, v in c['overlap'].items()},
         attack_mapping={int(k): set(v) for k, v in c['attack_mapping'].items()},
@@ -371,7 +459,7 @@ def build_reference_env(c):
         observe_self=c['observe_self'],
         no_overlap_at_reset=c['no_overlap_at_reset'],
         randomize_placement_order=c.get('randomize_placement_order', False),
-        states={'PositionState', 'HealthState'},
+        states={'PositionState', 'HealthState'} | ({'AmmoState'} if c.get('ammo') else set()),
         observers={'PositionCenteredEncodingObserver'},
         dones=set(c['dones']))
     if 'target_mapping' in c:
@@ -385,11 +473,16 @@ def build_reference_env(c):
             arr, {'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=wenc, blocking=True)},
             extra_agents=agents, **kwargs)
     else:
-        sim = TeamBattleSim.build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
+        sim_cls = TeamBattleSim
+        if c.get('len_fix'):
+            sim_cls = len_fixed_team_battle(TeamBattleSim)
+        sim = sim_cls.build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
     # pin the set-ordered state components (smart.py:37)
     pos = [s for s in sim._states if isinstance(s, PositionState)][0]
     hea = [s for s in sim._states if isinstance(s, HealthState)][0]
-    sim._states = [pos, hea] if c['state_order'] == 'position_health' else [hea, pos]
+    ammo = [s for s in sim._states if isinstance(s, AmmoState)]
+    # AmmoState draws nothing: its place in the order changes no result
+    sim._states = ([pos, hea] if c['state_order'] == 'position_health' else [hea, pos]) + ammo
     return AllStepManager(sim, randomize_action_input=c.get('randomize_action_input', False))
 
 
@@ -440,6 +533,7 @@ def run_case(case):
         reset_mask=np.zeros((T, E), dtype=np.uint8),
         err=np.zeros((T, E), dtype=np.uint8),
         reset_obs=np.full((T, E, A, S, S), -2, dtype=np.int8),
+        ammo=np.zeros((T, E, A), dtype=np.int16),
     )
     steps = [0] * E
     for t in range(T):
@@ -491,6 +585,7 @@ def run_case(case):
                 out['pos'][t, e, i] = agent.position
                 out['health'][t, e, i] = getattr(agent, 'health', 0.0)
                 out['active'][t, e, i] = int(agent.active)
+                out['ammo'][t, e, i] = getattr(agent, 'ammo', 0)
             out['all_done'][t, e] = int(bool(d['__all__']))
             st = np.random.get_state()
             out['mt_pos'][t, e] = st[2]

@@ -27,6 +27,8 @@ def check_step(g, t, obs, rew, done, all_done, state=None, where='', errors=None
             g['pos'][t][err] = state['pos'][err]
             g['health'][t][err] = state['health'][err]
             g['active'][t][err] = ((state['flags'] >> 2) & 1)[err]
+            if 'ammo' in g and 'ammo' in state:
+                g['ammo'][t][err] = state['ammo'][err]
     ok_obs = obs.astype(np.int64) == g['obs'][t].astype(np.int64)
     assert ok_obs.all(), f"{where} step {t}: obs mismatch at {np.argwhere(~ok_obs)[:5].tolist()}"
     bad = _bits(rew) != _bits(g['reward'][t])
@@ -40,6 +42,8 @@ def check_step(g, t, obs, rew, done, all_done, state=None, where='', errors=None
         assert (h == g['health'][t]).all(), f"{where} step {t}: health differs"
         act = (state['flags'] >> 2) & 1
         assert (act == g['active'][t]).all(), f"{where} step {t}: active differs"
+        if 'ammo' in g and 'ammo' in state:
+            assert (state['ammo'] == g['ammo'][t]).all(), f"{where} step {t}: ammo differs"
         mt = state['mt']
         for e in range(E):
             assert int(mt[e, 624]) == int(g['mt_pos'][t, e]), f"{where} step {t} env {e}: RNG pos"

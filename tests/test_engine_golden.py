@@ -63,6 +63,7 @@ class EngineRunner:
         out['pos'] = pos
         out['health'] = self._ent(out['health'], 0.0)
         out['flags'] = self._ent(out['flags'], 0x5)    # in grid, active
+        out['ammo'] = self._ent(self.eng.get_ammo().cpu().numpy(), 0)
         return out
 
     def errors(self):

@@ -29,7 +29,9 @@ class OracleRunner:
         return self.obs, self.rew, self.done, self.all_done
 
     def state(self):
-        return self.o.state()
+        st = self.o.state()
+        st['ammo'] = self.o.ammo()
+        return st
 
     def errors(self):
         return self.o.errors()
