@@ -134,7 +134,6 @@ struct Params {
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
     int32_t pair_cap;                      // crowded (observer, cell) pairs that fit after the obs stage
-    int32_t nact_off;                      // parked next-step actions: offset in the work area
     int32_t act_dim;                       // ints per entity action (gw_config_act_dim)
     int32_t attack_kind;                   // GW_ATTACK_*
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
@@ -269,12 +268,7 @@ __device__ __forceinline__ void buf_store_i8x4(__amdgpu_buffer_rsrc_t rs, uint32
     asm("v_max_i32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
         : "=v"(v3) : "v"(w), "v"(m2));
     const u32x4 v = {(uint32_t)v0, (uint32_t)v1, (uint32_t)v2, (uint32_t)v3};
-#ifdef GW_AB_NO_OBS_GSTORE
-    asm volatile("" :: "v"(v), "v"(voff));
-    (void)rs; (void)ioff;
-#else
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)voff + ioff, 0, GW_OBS_STORE_AUX);
-#endif
 }
 
 // The kernel's Params (its only / first argument, at kernarg offset 0) read
@@ -664,7 +658,6 @@ struct Smem {
     uint32_t* tcnt;
     uint32_t* scnt;
     int8_t* stage;
-    int32_t* nact;          // step kernel: the next step's actions [64][3] (gw_rollout)
 };
 
 // Jacobi placement scratch in the work area (do_reset): stream words,
@@ -683,15 +676,10 @@ constexpr size_t JAC_WORK_BYTES = JAC_OFF_KEY2 + 4 * GW_MT_N;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// the step kernel's parked next-step actions [64][3] (gw_rollout) sit at the
-// end of the work area: after the observation stage and its crowded-pair
-// list, clobbered by a reset's placement (the kernel then re-reads them)
-constexpr size_t NACT_BYTES = WAVE * 3 * 4;
-
 __host__ __device__ inline size_t work_bytes(int HW, int A, int S, int max_enc)
 {
     size_t w = 2 * align16((size_t)((HW + 3) / 4) * 4);
-    size_t s = align16((size_t)A * S * ((S + 3) & ~3)) + NACT_BYTES;     // observation stage [A][S][SP]
+    size_t s = align16((size_t)A * S * ((S + 3) & ~3));     // observation stage [A][S][SP]
     (void)max_enc;
     if (s < w) s = w;
     return s > JAC_WORK_BYTES ? s : JAC_WORK_BYTES;
@@ -713,7 +701,6 @@ __device__ __forceinline__ Smem carve(char* base, const Params& p)
     s.tcnt = (uint32_t*)base;
     s.scnt = (uint32_t*)(base + align16((size_t)((HW + 3) / 4) * 4));
     s.stage = (int8_t*)base;
-    s.nact = (int32_t*)(base + p.nact_off);
     return s;
 }
 
@@ -2289,17 +2276,6 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_PRIO_RESET_W
 #define GW_PRIO_RESET_W 192
 #endif
-// issue priority of a step kernel wave in gw_rollout: 1 by progress through
-// the fragment, 2 by remaining work (measured +2.8 % on the driver's
-// command, profiles/r03/ab_prio_remaining_work.jsonl)
-#ifndef GW_PROGRESS_PRIO
-#define GW_PROGRESS_PRIO 2
-#endif
-// next-step actions loaded ahead and parked in LDS: measured 2 % slower per
-// 100-step fragment on the round-3 kernel (profiles/r03/ab_head_prefetch.jsonl)
-#ifndef GW_PREFETCH_ACTIONS
-#define GW_PREFETCH_ACTIONS 0
-#endif
 // lane_step_kernel: steps of actions in flight ahead of the step (gw_lane.inc)
 #ifndef GW_LANE_PD
 #define GW_LANE_PD 4
@@ -2352,24 +2328,20 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     // the LDS table holds the template (load_env); lanes are added before
     // the first step that needs them (a reset adds its own)
     bool lanes_in = false, need_tmpl = false;
-    int pa0 = 0, pa1 = 0, pa2 = 0;             // actions of step t + 1 (prefetched)
-    bool nact_ok = false;                       // sm.nact holds them
     for (int t = 0; t < p.nsteps; t++) {
 #if GW_FRESH_PARAMS
         const Params& p = kernel_params();
 #endif
-        // progress priority (gw_rollout): the four envs of a SIMD start
-        // together, and VALU issue goes by priority, then age, so the youngest
-        // wave would trail the others and end the launch alone; a wave drops
-        // one level per quarter of the fragment it has done, so the SIMD's
-        // waves stay within about a quarter of each other
+        // issue priority (gw_rollout): the four envs of a SIMD start together,
+        // and VALU issue goes by priority, then age, so a heavy young wave
+        // would trail the others and end the launch alone.  Remaining-work
+        // priority: the wave's remaining agent-steps in this fragment (live
+        // agents x steps left, a pending horizon reset counted as
+        // GW_PRIO_RESET_W agent-steps) against a typical env's (~24 live
+        // agents): the SIMD issues the heaviest env first (measured +2.8 %
+        // on the driver's command, profiles/r03/ab_prio_remaining_work.jsonl)
         int prio = 0;
-        if (GW_PROGRESS_PRIO == 1 && p.nsteps > 1) prio = 3 - min(3, (4 * t) / p.nsteps);
-        if (GW_PROGRESS_PRIO == 2 && p.nsteps > 1) {
-            // remaining-work priority: the wave's remaining agent-steps in this
-            // fragment (live agents x steps left, a pending horizon reset
-            // counted as GW_PRIO_RESET_W agent-steps) against a typical env's
-            // (~24 live agents): the SIMD issues the heaviest env first
+        if (p.nsteps > 1) {
             const int left = p.nsteps - t;
             const int nlive = __popcll(__ballot(valid && L.live));
             const bool rpend = p.horizon > 0 && steps + left >= p.horizon;
@@ -2384,29 +2356,14 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         double* rew_t = p.reward + (size_t)t * EA;
         uint8_t* done_t = p.done + (size_t)t * EA;
         uint8_t* ad_t = p.all_done + (size_t)t * p.E;
-        // the next step's actions are loaded at the top of this step, before
-        // this step's stores (vmcnt counts loads and stores in issue order: a
-        // load issued at the top of step t+1 would wait for step t's stores as
-        // well), and parked in LDS (sm.nact) once the step's first passes are
-        // done, so that they hold no registers through the observation
-        if (t > 0 && (!GW_PREFETCH_ACTIONS || !nact_ok)) {
+        // this step's actions (step 0's came with the prologue); loading the
+        // next step's ahead and parking them in LDS measured 2 % slower per
+        // 100-step fragment (profiles/r03/ab_head_prefetch.jsonl)
+        if (t > 0) {
             const int32_t* ap = act_t + act_row;
             const int a0 = ap[0], a1 = ap[1], a2 = ap[2];
             mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
-        } else if (t > 0) {
-            const int32_t* na = sm.nact + 3 * l;
-            const int a0 = na[0], a1 = na[1], a2 = na[2];
-            mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
         }
-        const bool prefetch = GW_PREFETCH_ACTIONS && t + 1 < p.nsteps;
-        if (prefetch) {
-            const int32_t* ap = act_t + (size_t)EA * p.act_dim + act_row;
-            pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
-        }
-        nact_ok = false;
-        auto park = [&]() {
-            if (prefetch) { int32_t* na = sm.nact + 3 * l; na[0] = pa0; na[1] = pa1; na[2] = pa2; nact_ok = true; }
-        };
         if (need_tmpl) { table_template(p, sm); lanes_in = false; need_tmpl = false; }
         // NEXT_STEP auto-reset: the episode ended in the previous step, so this
         // step is AllStepManager.reset for the env (actions ignored): obs =
@@ -2662,7 +2619,6 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 }
             }
             STAMP(3);
-            park();
             if (raised) {
                 // Grid.remove raised KeyError: the step stops here (no further
                 // moves, no observation draws, its outputs are not written); the
@@ -2680,9 +2636,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
 
                 // ---- observations of the live agents (all_step_manager.py:68-71)
                 STAMP(4);
-#ifndef GW_AB_NO_OBS
                 observe_all<S, PLAIN>(p, e, sm, rng, L, obs_t);
-#endif
                 STAMP(5);
 
                 // ---- rewards, dones (:72-79, smart.py:101-111)
@@ -2736,9 +2690,6 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             }
         }
         if (reset_now) {
-            // (the placement's scratch overlaps the parked actions: the next
-            // step re-reads its actions from memory)
-            nact_ok = false;
             // the reset is the launch's critical path: issue it ahead of the
             // SIMD's stepping waves
             __builtin_amdgcn_s_setprio(3);
@@ -3805,9 +3756,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             p.hsmask = g->d_hsmask;
         }
     }
-    p.pair_cap = (int)((work_bytes(HW, A, Sst, max_enc) - NACT_BYTES -
-                        (size_t)A * Sst * ((Sst + 3) & ~3)) / 2);
-    p.nact_off = (int32_t)(work_bytes(HW, A, Sst, max_enc) - NACT_BYTES);
+    p.pair_cap = (int)((work_bytes(HW, A, Sst, max_enc) - (size_t)A * Sst * ((Sst + 3) & ~3)) / 2);
     g->smem_step = smem_bytes(HW, A, Sst, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
         // pac_carve: cval | pb | clist | cp | penc
