@@ -141,8 +141,18 @@ class ComponentRuntime:
         cc.cfg.component_api = 1
         # every entity a lane: the maze placements place every entity, and a
         # grid of static entities only has no lane to run on
-        cc.cfg.all_lanes = 1 if sig[5] or not any(
-            not self._static(a, s_, grid, sig) for a, s_ in zip(agents.values(), specs)) else 0
+        static = [self._static(a, s_, grid, sig) for a, s_ in zip(agents.values(), specs)]
+        # a static entity whose initial cell another entity's initial position
+        # also names: the reference's reset raises (Grid.place refuses), which
+        # the lanes reproduce -- the cell template cannot hold both
+        cells = {}
+        for a in agents.values():
+            if a.initial_position is not None:
+                rc = (int(a.initial_position[0]), int(a.initial_position[1]))
+                cells[rc] = cells.get(rc, 0) + 1
+        clash = any(st and cells[(int(a.initial_position[0]), int(a.initial_position[1]))] > 1
+                    for st, a in zip(static, agents.values()))
+        cc.cfg.all_lanes = 1 if sig[5] or clash or not any(not st for st in static) else 0
         self.cc = cc
         try:
             self.eng = GridWorldEngine(cc, 1, seeds=[0])
