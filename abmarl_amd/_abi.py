@@ -172,7 +172,7 @@ class CompiledConfig:
             cfg.tunnel[i] = int(tunnel[i])
         for i in range(5):
             cfg.pac_rewards[i] = float(pac_rewards[i])
-        cfg.force_workgroup = int(bool(force_workgroup))
+        cfg.force_workgroup = int(force_workgroup)   # 0 auto, 1 workgroup kernel, 2..4 waves per env
         self.cfg = cfg
         self.rows, self.cols = rows, cols
         self.obs_kind = obs_kind

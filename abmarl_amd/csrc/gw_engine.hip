@@ -3517,6 +3517,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     const bool wg_able = (rtt && cfg->attack_kind == GW_ATTACK_SELECTIVE) ||
                          (tb && cfg->attack_kind == GW_ATTACK_BINARY) ||
                          (cfg->component_api && (rtt || tb));
+    if (cfg->force_workgroup < 0 || cfg->force_workgroup > GW_MAX_LANES / WAVE) {
+        set_err("force_workgroup %d: 0 (automatic), 1 (workgroup kernel) or 2..%d waves per env",
+                cfg->force_workgroup, GW_MAX_LANES / WAVE);
+        return GW_E_INVALID;
+    }
     if (cfg->force_workgroup && !wg_able) {
         set_err("force_workgroup: the workgroup-per-env kernel runs ReachTheTarget with SelectiveAttackActor "
                 "and TeamBattle with BinaryAttackActor");
@@ -3837,8 +3842,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     }
     g->smem_reset = g->smem_step;
     if (wg) {
+        // force_workgroup >= 2 asks for that many waves (the extra threads
+        // share the table, observation store and crowded-draw work)
         p.nwv = (A + WAVE - 1) / WAVE;
-        g->smem_step = g->smem_reset = wg_smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch);
+        if (cfg->force_workgroup > p.nwv) p.nwv = cfg->force_workgroup;
+        g->smem_step = g->smem_reset = wg_smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch, p.nwv);
         // moves run in parallel when every moving lane's encoding may share a
         // cell with every lane encoding (static cells are refused separately)
         uint32_t lane_encs = 0;

@@ -285,11 +285,25 @@ def quick_config(name, steps=200, warmup=400):
         torch.cuda.synchronize()
         rdt = time.perf_counter() - t1
         ra = int(eng.acting.sum().item()) - r0
+        lms = float(np.mean([a.elapsed_time(b) for a, b in revs]))
+        rb = rollout_bytes(E, eng.A, cc.obs_side, F, ra / len(revs), eng.act_dim)
         roll = {'value': round(ra / rdt, 1), 'ms_per_step': round(rdt / ((NF - 1) * F) * 1e3, 4),
-                'launch_ms': round(float(np.mean([a.elapsed_time(b) for a, b in revs])), 4),
-                'steps_per_launch': F,
+                'launch_ms': round(lms, 4), 'steps_per_launch': F, 'bytes_per_launch': round(rb),
+                'achieved_GBs': round(rb / (lms * 1e-3) / 1e9, 2),
                 'protocol': 'gw_rollout fragments of 100 steps on actions resident in HBM (after an '
                             'untimed first fragment), launch events recorded by the dispatch'}
+        kn = {'maze': 'lane_step_kernel', 'rtt': 'wg_step_kernel', 'rtt_8192': 'wg_step_kernel'}[name]
+        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kn}_rollout_f{F}.json')
+        if os.path.exists(pmc):
+            # the committed PMC evidence of this launch shape (tools/prof_headline.sh
+            # <tag> rtt, tools/profile.sh maze): HBM bytes over the algorithmic
+            # bytes of the SAME profiled launch
+            prof = json.load(open(pmc))
+            if prof.get('algorithmic_bytes_per_launch') and prof.get('hbm_bytes_per_launch') and \
+                    (name != 'rtt_8192' or prof.get('envs') == 8192):
+                roll['traffic'] = round(prof['hbm_bytes_per_launch'])
+                roll['traffic_ratio'] = round(prof['hbm_bytes_per_launch'] / prof['algorithmic_bytes_per_launch'], 4)
+                roll['traffic_source'] = f'profiles/{os.path.basename(pmc)} ({prof.get("tag")})'
     if name == 'maze':
         nbytes = step_bytes(E, eng.A, cc.obs_side)
         desc = ('MazeNavigation 16x16 (workloads.MAZE_16), 1024 envs, AllStep, next_step auto-reset '
@@ -359,6 +373,10 @@ def main():
     ap.add_argument('--workload', choices=sorted(WORKLOADS), default='team_battle',
                     help="the timed workload; the metric's is team_battle (BASELINE configs[2]); the "
                          "others are BASELINE configs 2, 4, 5 (their own lines, not the headline metric)")
+    ap.add_argument('--workgroup-waves', type=int, default=0,
+                    help='team_battle: run on the workgroup-per-env kernel with this many waves per '
+                         'env (2-4; the small-batch variant, gw_config.force_workgroup); 0: the '
+                         'one-wave kernel')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -376,6 +394,10 @@ def main():
     builder, default_envs, kname, wdesc = WORKLOADS[args.workload]
     sim = builder()
     cc = sim.compiled()
+    if args.workgroup_waves:
+        cc.cfg.force_workgroup = args.workgroup_waves
+        kname = 'wg_step_kernel<7>'
+        wdesc += f' (workgroup kernel, {args.workgroup_waves} waves per env)'
     turn = args.workload == 'pacman'
     strong = args.global_envs > 0
     total_envs = args.global_envs if strong else (args.envs or default_envs) * world
@@ -592,7 +614,7 @@ def main():
         # rollout profile is per fragment length: tools/profile.sh ... <F>)
         pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{f"_rollout_f{F}" if rollout else ""}.json')
         prof = {}
-        if args.workload in ('team_battle', 'maze') and os.path.exists(pmc):
+        if args.workload in ('team_battle', 'maze', 'rtt') and not args.workgroup_waves and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')
             rocprof_ms = prof.get('rocprof_avg_ms')

@@ -209,7 +209,10 @@ typedef struct gw_config {
     /* kernel selection: 0 = automatic (one wave per env; ReachTheTarget with
        more than GW_MAX_AGENTS lanes on a workgroup per env), 1 = force the
        workgroup-per-env kernel (ReachTheTarget; parity tests run the small
-       reference fixtures through it)                                         */
+       reference fixtures through it), 2..4 = the workgroup kernel with that
+       many waves per env (at least ceil(lanes / 64)): the threads past the
+       lanes share the table, observation-store and crowded-draw work (small
+       batches: more waves per env when there are fewer envs than SIMDs)     */
     int32_t  force_workgroup;
     /* 1: the caller passes the SAME obs buffer to every call of this handle
        (as the Python engine does with its own), so the one-wave kernels do

@@ -117,6 +117,16 @@ def test_dense_configs_workgroup_kernel(oracle_mod, idx):
     _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, force_workgroup=True)
 
 
+@pytest.mark.parametrize('waves', [2, 4])
+def test_headline_config_multi_wave(oracle_mod, waves):
+    """The headline TeamBattle config on the workgroup kernel with 2 and 4
+    waves per env (gw_config.force_workgroup = waves: the small-batch
+    variant; threads past the 64 lanes share the table, store and crowded
+    draws) vs the oracle."""
+    cc = team_battle()
+    _run(oracle_mod, cc, E=512, T=120, horizon=50, seed_run=3, key=17, check_every=2, force_workgroup=waves)
+
+
 @pytest.mark.parametrize('kernel', ['lane', 'wave'])
 def test_maze_navigation_1024_envs(oracle_mod, kernel):
     """BASELINE config 2: MazeNavigation 16x16 (generate_maze walls, blocking),

@@ -200,6 +200,26 @@ def test_rollout_workgroup_team_battle():
     _compare(a, b, 0, horizon=30, mode='same_step', frags=(15,))
 
 
+@pytest.mark.parametrize('waves', [2, 4])
+def test_rollout_multi_wave_team_battle(waves):
+    """The headline TeamBattle config on the workgroup kernel with 2 / 4
+    waves per env (the small-batch variant) as fragments vs single steps."""
+    cc = team_battle()
+    a, b = _pair(cc, 256, run=10, stagger=30, force_workgroup=waves)
+    assert a.wg
+    _compare(a, b, 0, horizon=30, mode='next_step', frags=(20, 20), skip=True)
+    _compare(a, b, 0, horizon=30, mode='same_step', frags=(15,))
+
+
+def test_rollout_multi_wave_double_remove():
+    """A crowded ReachTheTarget case (fewer than 64 lanes) on 4 waves."""
+    from tests.test_engine_oracle import RTT_WAVE_CASES
+    cc = build_rtt(dict(kind='rtt', **RTT_WAVE_CASES[1])).compiled()
+    a, b = _pair(cc, 256, run=6, force_workgroup=4)
+    assert a.wg
+    _compare(a, b, 0, horizon=40, mode='next_step', frags=(25, 25), allow_err=True)
+
+
 def test_rollout_traffic_corridor():
     from tests.cases import build_traffic
     cc = build_traffic(load_golden('traffic_9')['case']).compiled()

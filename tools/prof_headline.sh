@@ -2,7 +2,8 @@
 # rocprofv3 evidence for the headline line, on the GPU box, at the driver's
 # own workload (bench.py --gpus 1 --steps 20 --warmup 5: 1000-step pre-roll,
 # ONE timed 20-step gw_rollout launch):
-#   bash tools/prof_headline.sh <tag>   -> gpurun_out/ph_<tag>/
+#   bash tools/prof_headline.sh <tag> [rtt]   -> gpurun_out/ph_<tag>/
+# (rtt: BASELINE config 4's line, bench.py --workload rtt --steps 100 --warmup 5)
 # 1. --kernel-trace --stats over the driver's exact command;
 # 2. FETCH_SIZE and WRITE_SIZE, one --pmc pass each, same workload with the
 #    other configs and the CPU baseline skipped (--no-other --no-cpu-baseline:
@@ -16,7 +17,12 @@ TAG=${1:?tag}
 OUT=gpurun_out/ph_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 bench.py --gpus 1 --steps 20 --warmup 5"
+WL=${2:-team_battle}
+if [ "$WL" = rtt ]; then
+  CMD="python3 bench.py --gpus 1 --workload rtt --steps 100 --warmup 5"
+else
+  CMD="python3 bench.py --gpus 1 --steps 20 --warmup 5"
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- $CMD \
     > $OUT/stats.log 2>&1 || { echo "stats pass failed"; tail -20 $OUT/stats.log; exit 1; }
 SHORT="$CMD --no-other --no-cpu-baseline"
@@ -29,4 +35,4 @@ for SET in FETCH_SIZE WRITE_SIZE \
   timeout -s KILL 150 rocprofv3 --pmc $SET --output-format csv -d $OUT/p$i -o run -- $SHORT \
       > $OUT/p$i.log 2>&1 || { echo "PMC pass $i ($SET) failed"; tail -20 $OUT/p$i.log; exit 1; }
 done
-python3 tools/summarize_headline.py $TAG --raw $OUT --dest $OUT/profiles
+python3 tools/summarize_headline.py $TAG --raw $OUT --dest $OUT/profiles --workload $WL

@@ -15,7 +15,11 @@ Dispatch order: bench.py's run_rollout launches the pre-roll + warmup
 the timed 20-step launch; so in the first engine's run the step_kernel
 dispatches are [100] * 9 + [85, 20] and then the timed one (index 11).
 
-usage: python tools/summarize_headline.py <tag> --raw DIR --dest DIR
+--workload rtt: the same for BASELINE config 4's line (bench.py --workload
+rtt --steps 100 --warmup 5: wg_step_kernel<7>, 1024 envs, one timed 100-step
+launch; <tag>_rtt_* and pmc_wg_step_kernel_rollout_f100.json).
+
+usage: python tools/summarize_headline.py <tag> --raw DIR --dest DIR [--workload rtt]
 """
 import argparse
 import csv
@@ -27,8 +31,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# workload: (kernel, envs, entity slots, obs side, fragment steps, action ints
+# per slot, bench.py arguments)
+WORKLOADS = {
+    'team_battle': ('step_kernel<7, 1>', 4096, 64, 7, 20, 3, '--gpus 1 --steps 20 --warmup 5'),
+    'rtt': ('wg_step_kernel<7>', 1024, 256, 7, 100, 11, '--gpus 1 --workload rtt --steps 100 --warmup 5'),
+}
 KERNEL = 'step_kernel<7, 1>'
 E, A, S, F, ACT_DIM = 4096, 64, 7, 20, 3
+BENCH_ARGS = WORKLOADS['team_battle'][6]
 
 
 def short(name):
@@ -89,13 +100,17 @@ def main():
     ap.add_argument('tag')
     ap.add_argument('--raw', required=True)
     ap.add_argument('--dest', required=True)
+    ap.add_argument('--workload', default='team_battle', choices=sorted(WORKLOADS))
     a = ap.parse_args()
+    global KERNEL, E, A, S, F, ACT_DIM, BENCH_ARGS
+    KERNEL, E, A, S, F, ACT_DIM, BENCH_ARGS = WORKLOADS[a.workload]
+    kind = 'headline' if a.workload == 'team_battle' else a.workload
     from bench import rollout_bytes
     os.makedirs(a.dest, exist_ok=True)
-    sizes = fragments()
+    sizes = fragments(steps=F)
     ti = len(sizes)                          # index of the timed dispatch
     st = os.path.join(a.raw, 'stats')
-    shutil.copy(find(st, '*kernel_stats.csv'), os.path.join(a.dest, f'{a.tag}_headline_kernel_stats.csv'))
+    shutil.copy(find(st, '*kernel_stats.csv'), os.path.join(a.dest, f'{a.tag}_{kind}_kernel_stats.csv'))
     line = bench_line(os.path.join(a.raw, 'stats.log'))
     rows = trace(st)
     sk = [i for i, r in enumerate(rows) if short(r['Kernel_Name']) == KERNEL]
@@ -124,9 +139,9 @@ def main():
     sq = {k: v[ti] for k, v in p.items() if k.startswith('SQ_')}
     waves = sq.get('SQ_WAVES') or 1.0
     pmc = {
-        'tag': a.tag, 'kernel': KERNEL,
-        'workload_args': 'bench.py --gpus 1 --steps 20 --warmup 5 (--no-other --no-cpu-baseline for '
-                         'the PMC passes): 1000-step pre-roll, the timed 20-step gw_rollout launch',
+        'tag': a.tag, 'kernel': KERNEL, 'envs': E,
+        'workload_args': f'bench.py {BENCH_ARGS} (--no-other --no-cpu-baseline for '
+                         f'the PMC passes): 1000-step pre-roll, the timed {F}-step gw_rollout launch',
         'dispatch_index': ti, 'resources': res,
         'acting_agent_steps': acting,
         'algorithmic_bytes_per_launch': alg,
@@ -141,25 +156,25 @@ def main():
         'steps_per_launch': F, 'mode': 'rollout',
         'sq_timed_launch': sq,
     }
-    json.dump(pmc, open(os.path.join(a.dest, 'pmc_step_kernel_rollout_f20.json'), 'w'), indent=1)
+    json.dump(pmc, open(os.path.join(a.dest, f'pmc_{KERNEL.split("<")[0]}_rollout_f{F}.json'), 'w'), indent=1)
     roof = line.get('roofline', {})
-    L = [f'# Headline profile `{a.tag}`: the driver\'s workload', '',
+    L = [f'# {kind} profile `{a.tag}`' + (': the driver\'s workload' if kind == 'headline' else ''), '',
          'Command (kernel trace): `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py '
-         '--gpus 1 --steps 20 --warmup 5`; PMC: one `--pmc` pass per counter set, the same command with '
+         f'{BENCH_ARGS}`; PMC: one `--pmc` pass per counter set, the same command with '
          '`--no-other --no-cpu-baseline` (tools/prof_headline.sh).', '',
          f'## {KERNEL} dispatches of the headline engine (stats run)', '',
          '| # | steps | duration us |', '|---|---|---|']
     for k, i in enumerate(sk[:ti + 1]):
         L.append(f'| {k} | {sizes[k] if k < ti else str(F) + " (TIMED)"} | {dur(i):.1f} |')
     L += ['',
-          f'- timed launch: **{dur(timed):.1f} us** (rocprof); the untimed 20-step launch right before it: '
+          f'- timed launch: **{dur(timed):.1f} us** (rocprof); the untimed {F}-step launch right before it: '
           f'{dur(prev_frag):.1f} us; the same_step engine\'s timed launch: '
           f'{(dur(timed2) if timed2 is not None else float("nan")):.1f} us',
           f'- idle gap before the timed launch (after `{prev_name}` ended): {gap:.1f} us '
           '(host: synchronize, acting read-back, synchronize, event record, launch)',
           f'- the same run\'s HIP-event launch time (bench line `roofline.kernel_ms`): '
           f'{roof.get("kernel_ms")} ms; '
-          f'wall ms_per_step x 20: {line.get("ms_per_step", 0) * 20:.4f} ms; value {line.get("value"):.4g}',
+          f'wall ms_per_step x {F}: {line.get("ms_per_step", 0) * F:.4f} ms; value {line.get("value"):.4g}',
           f'- resources: `{res}`', '',
           '## Traffic of the timed launch (PMC run)', '',
           f'- acting agent-steps in the launch: {acting}',
@@ -178,7 +193,7 @@ def main():
                   f'{sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_LDS_IDX_ACTIVE"]:.3f}']
     if 'SQ_WAIT_ANY' in sq and sq.get('SQ_WAVE_CYCLES'):
         L += [f'wave cycles waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES): {sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]:.3f}']
-    open(os.path.join(a.dest, f'{a.tag}_headline_summary.md'), 'w').write('\n'.join(L) + '\n')
+    open(os.path.join(a.dest, f'{a.tag}_{kind}_summary.md'), 'w').write('\n'.join(L) + '\n')
     print('\n'.join(L))
 
 
