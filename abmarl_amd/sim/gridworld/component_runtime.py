@@ -27,7 +27,9 @@ BASELINE config-4 grid of 256 entities).
 
 Host <-> device traffic per call is kept small: the state is uploaded only
 when the host changed it since the last call (agent / Grid setters bump
-sim/host_version.py; the numpy stream is compared word for word), in-cell
+sim/host_version.py; the numpy stream is compared word for word, and the
+lane agents' position / active / health / ammo values against what the last
+call left, which catches in-place array edits), in-cell
 order goes up as per-cell ranks, and the download rewrites only the Grid
 cells whose occupants moved.
 """
@@ -177,6 +179,7 @@ class ComponentRuntime:
         # stream, and the entities' (in grid, row, col, seq) for the mirror
         self._synced = None
         self._where = None
+        self._fp = None
 
     @staticmethod
     def _static(agent, spec, grid, sig):
@@ -300,13 +303,26 @@ class ComponentRuntime:
         self._where = (inside, pos.copy(), seq.copy())
         s = np.random.get_state()
         self._synced = (host_version.VERSION[0], s[2], s[1].copy(), s[3], s[4])
+        self._fp = self._fingerprint()
+
+    def _fingerprint(self):
+        """The lane agents' position / active / health / ammo values as the
+        host holds them: an in-place edit (an element of a position or health
+        array) bumps no version, so op() compares this too."""
+        out = []
+        for a in self.lane_agents:
+            p = a.position
+            out.append((None if p is None else (int(p[0]), int(p[1])), bool(a.active),
+                        getattr(a, '_health', None), getattr(a, '_ammo', None)))
+        return out
 
     # ----------------------------------------------------------- operations
     def op(self, op, agent=None, args=None):
         """Run one component operation; returns (status, attacked agents, err)
         (the raw result row stays in self.last_result)."""
         lane = -1 if agent is None else self.index[agent.id]
-        if self._synced is None or self._synced[0] != host_version.VERSION[0] or not self._rng_matches():
+        if self._synced is None or self._synced[0] != host_version.VERSION[0] or not self._rng_matches() or \
+                self._fingerprint() != self._fp:
             self._upload()
         if args is not None:
             a = np.zeros((1, self.eng.act_dim), np.int32)

@@ -198,6 +198,54 @@ def test_move_actor_with_overlap():
     assert set(grid[2, 2]) == {'agent1', 'agent3'}
 
 
+@gpu
+def test_static_wall_edited_on_the_host():
+    """A wall (a static entity: the engine keeps it in its cell template) that
+    the host removes through Grid.remove stops blocking, and one the host
+    places elsewhere blocks there: the runtime sees the edit and rebuilds
+    with every entity a lane (reference semantics: Grid.query on the host's
+    cells, grid.py:81-140)."""
+    grid = Grid(3, 3)
+    agents = {'mover': MovingAgent(id='mover', initial_position=np.array([1, 0]), encoding=1, move_range=1),
+              'wall': GridWorldAgent(id='wall', initial_position=np.array([1, 1]), encoding=3)}
+    ps = PositionState(grid=grid, agents=agents)
+    move = MoveActor(grid=grid, agents=agents)
+    ps.reset()
+    mover, wall = agents['mover'], agents['wall']
+    assert not move.process_action(mover, {'move': np.array([0, 1])})     # the wall blocks
+    np.testing.assert_array_equal(mover.position, [1, 0])
+    grid.remove(wall, (1, 1))
+    assert move.process_action(mover, {'move': np.array([0, 1])})         # now the cell is empty
+    np.testing.assert_array_equal(mover.position, [1, 1])
+    assert grid.place(wall, (1, 2))
+    assert not move.process_action(mover, {'move': np.array([0, 1])})     # blocked at its new cell
+    np.testing.assert_array_equal(mover.position, [1, 1])
+    assert move.process_action(mover, {'move': np.array([-1, 0])})
+    np.testing.assert_array_equal(mover.position, [0, 1])
+    assert set(grid[1, 2]) == {'wall'} and not grid[1, 1]
+
+
+@gpu
+def test_in_place_host_edit_is_seen():
+    """Edits that bump no host version -- an element of an agent's position
+    array and the Grid's cell dicts written directly -- still reach the
+    device before the next component call (the runtime's fingerprint)."""
+    grid = Grid(4, 4)
+    agents = {'mover': MovingAgent(id='mover', initial_position=np.array([1, 0]), encoding=1, move_range=1)}
+    ps = PositionState(grid=grid, agents=agents)
+    move = MoveActor(grid=grid, agents=agents)
+    ps.reset()
+    mover = agents['mover']
+    assert move.process_action(mover, {'move': np.array([1, 0])})
+    np.testing.assert_array_equal(mover.position, [2, 0])
+    del grid[2, 0]['mover']
+    grid[2, 2]['mover'] = mover
+    mover.position[1] = 2                                               # in place: (2, 2)
+    assert move.process_action(mover, {'move': np.array([-1, 0])})
+    np.testing.assert_array_equal(mover.position, [1, 2])
+    assert set(grid[1, 2]) == {'mover'} and not grid[2, 2] and not grid[2, 0]
+
+
 def _attack_agents(attacker_kw, health=None):
     h = {} if health is None else dict(initial_health=health)
     return {
