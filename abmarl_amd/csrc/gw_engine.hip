@@ -2389,9 +2389,33 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         mr = valid ? a0 : 0; mc = valid ? a1 : 0; ak = valid ? a2 : -1;
     }
     const uint64_t acting_raw = p.acting ? p.acting[e] : 0ull;
+    // the MT key with the prologue's loads (one round trip) when the launch
+    // runs several steps: nearly every env of a fragment draws beyond its
+    // cached block (crowded cells, placements), and a load on demand puts a
+    // memory round trip on that env's chain
+#ifndef GW_KEY_PREFETCH
+#define GW_KEY_PREFETCH 1
+#endif
+    const bool kpre = GW_KEY_PREFETCH == 2 || (GW_KEY_PREFETCH == 1 && p.nsteps > 1);
+    uint4 kq0 = {}, kq1 = {}, kq2 = {};
+    if (kpre) {
+        const uint4* ks = (const uint4*)(p.mt + (size_t)e * GW_MT_STRIDE);
+        constexpr int N4 = GW_MT_N / 4;
+        kq0 = ks[l];
+        kq1 = ks[l + WAVE];
+        kq2 = ks[l + 2 * WAVE < N4 ? l + 2 * WAVE : l];
+    }
     Rng rng;
     uint32_t ctr;
     load_env(p, e, sm, rng, ctr, true);
+    if (kpre) {
+        uint4* k4 = (uint4*)sm.key;
+        k4[l] = kq0;
+        k4[l + WAVE] = kq1;
+        if (l + 2 * WAVE < GW_MT_N / 4) k4[l + 2 * WAVE] = kq2;
+        wave_sync();
+        rng.loaded = true;
+    }
     int32_t steps = uni(steps_raw);
     uint64_t acting_sum = 0;
     bool prev_all = uni(ad_raw) != 0u;
