@@ -20,7 +20,7 @@ def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1, force_work
     cc.cfg.force_workgroup = int(force_workgroup)
     cc.cfg.env_per_lane = int(env_per_lane)
     eng = GridWorldEngine(cc, E, seeds=seeds)
-    assert eng.wg == (force_workgroup or eng.A > 64)
+    assert eng.wg == (bool(force_workgroup) or eng.A > 64)
     if kernel is not None:
         assert eng.kernel == kernel, (eng.kernel, kernel)
     orc = oracle_mod.Oracle(cc, E)
