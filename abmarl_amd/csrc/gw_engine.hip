@@ -2210,6 +2210,18 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         // lists some randomly placed lane draws from (the others are never read)
         const uint32_t draw_encs = wave_or((valid && L.init_r < 0) ? (1u << L.enc) : 0u);
+        // lists that every placement shortens together stay equal (TeamBattle:
+        // each team's list loses every placed cell): one register for them
+        const uint32_t rem_l = valid ? ((p.no_overlap_at_reset ? all_encs : (all_encs & ~L.ov)) & draw_encs) : 0u;
+        int rep[SORT_LISTS];
+#pragma unroll
+        for (int f = 0; f < SORT_LISTS; f++) {
+            rep[f] = f;
+            for (int g = f - 1; g >= 0; g--)
+                if (((draw_encs >> (g + 1)) & (draw_encs >> (f + 1)) & 1u) &&
+                    wave_or(((rem_l >> (f + 1)) ^ (rem_l >> (g + 1))) & 1u) == 0u)
+                    rep[f] = rep[g];
+        }
         const int32_t* order = p.place_order ? p.place_order + (size_t)blockIdx.x * A : nullptr;
         for (int pass = 0; pass < 2; pass++) {
             for (int k = 0; k < A; k++) {
@@ -2226,10 +2238,14 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     const bool blocks = valid && L.in_grid && cell_l == cell && !((aov >> L.enc) & 1u);
                     if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
                 } else {
+                    int fa = 0;
+#pragma unroll
+                    for (int f = 1; f < SORT_LISTS; f++)
+                        if (aenc == f + 1) fa = rep[f];
                     int Ra = R[0], ma = m[0];
 #pragma unroll
                     for (int f = 1; f < SORT_LISTS; f++)
-                        if (aenc == f + 1) { Ra = R[f]; ma = m[f]; }
+                        if (fa == f) { Ra = R[f]; ma = m[f]; }
                     const int n = NF - ma;
                     if (n <= 0) { err |= GW_ERR_NO_CELL; return false; }
                     const int idx = (int)rng.interval((uint32_t)(n - 1));   // np.random.choice(list, 1)
@@ -2240,7 +2256,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 const uint32_t rem = (p.no_overlap_at_reset ? all_encs : (all_encs & ~aov)) & draw_encs;
 #pragma unroll
                 for (int f = 0; f < SORT_LISTS; f++) {
-                    if (!((rem >> (f + 1)) & 1u)) continue;
+                    if (!((rem >> (f + 1)) & 1u) || rep[f] != f) continue;
                     if (__ballot(R[f] == cell)) continue;             // already removed
                     const int pos = __popcll(__ballot(R[f] < cell));
                     const int sh = (int)dpp<0x138>((uint32_t)R[f], (uint32_t)R[f]);   // wave_shr:1
