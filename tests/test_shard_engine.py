@@ -33,6 +33,16 @@ def _fragment(eng, key, t0, K, first):
     return acts
 
 
+def _run(eng, acts, horizon, skip):
+    """One fragment into fresh slabs pre-filled with the same byte pattern in
+    every engine: rows an env leaves unwritten (a step that raised: outputs
+    not written) then compare equal."""
+    out = eng.rollout_buffers(int(acts.shape[0]))
+    for v in out.values():
+        v.view(-1).view(__import__('torch').uint8).fill_(0xA5)
+    return eng.rollout(acts, horizon=horizon, skip_done_obs=skip, out=out)
+
+
 def _check_shards(cc, total, shards, horizon, frags, skip, key=0x5eed0000, allow_err=False):
     from abmarl_amd.parallel import shard_envs, gather_episode_stats
     whole = _engine(cc, 0, total, total, horizon)
@@ -43,9 +53,8 @@ def _check_shards(cc, total, shards, horizon, frags, skip, key=0x5eed0000, allow
     t = 0
     prev = None                # the previous step's done slab (whole engine)
     for K in frags:
-        out_w = whole.rollout(_fragment(whole, key, t, K, 0), horizon=horizon, skip_done_obs=skip)
-        outs = [(first, n, e.rollout(_fragment(e, key, t, K, first), horizon=horizon, skip_done_obs=skip))
-                for first, n, e in parts]
+        out_w = _run(whole, _fragment(whole, key, t, K, 0), horizon, skip)
+        outs = [(first, n, _run(e, _fragment(e, key, t, K, first), horizon, skip)) for first, n, e in parts]
         for s in range(K):
             for first, n, out in outs:
                 sl = slice(first, first + n)
