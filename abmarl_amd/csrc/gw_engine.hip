@@ -2186,93 +2186,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         return 0;
     };
 
-    // The same placement serially in placement order, with each list f kept
-    // as a SORTED register of the (free-space) cells removed from it: lane j
-    // holds the j-th smallest, m[f] of them.  np.random.choice(list, 1) draws
-    // the list index idx, and the listed cell is idx + #{j : R[j] - j <= idx}
-    // (the j-th removed cell has R[j] - j listed cells below it): one ballot.
-    // _update_available_positions inserts a cell the list still holds at its
-    // rank: one ballot for the rank, one DPP wave shift.  So a placement is
-    // a short fixed chain (a draw, a ballot, per shortened list two ballots
-    // and a shift) instead of the fixpoint iterations of the forms above.
-    // Lists of encodings that no randomly placed entity draws from are not
-    // kept.  Up to SORT_LISTS encodings (the Jacobi form beyond).
-    constexpr int SORT_LISTS = 4;
-#ifndef GW_SORTED_PLACE
-#define GW_SORTED_PLACE 1
-#endif
-    auto position_reset_sorted = [&]() -> bool {
-        constexpr int BIG = 0x7fffffff;
-        int R[SORT_LISTS], m[SORT_LISTS];
-#pragma unroll
-        for (int f = 0; f < SORT_LISTS; f++) { R[f] = BIG; m[f] = 0; }
-        int cell_l = -1;                 // this lane's cell once placed
-        const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
-        // lists some randomly placed lane draws from (the others are never read)
-        const uint32_t draw_encs = wave_or((valid && L.init_r < 0) ? (1u << L.enc) : 0u);
-        // lists that every placement shortens together stay equal (TeamBattle:
-        // each team's list loses every placed cell): one register for them
-        const uint32_t rem_l = valid ? ((p.no_overlap_at_reset ? all_encs : (all_encs & ~L.ov)) & draw_encs) : 0u;
-        int rep[SORT_LISTS];
-#pragma unroll
-        for (int f = 0; f < SORT_LISTS; f++) {
-            rep[f] = f;
-            for (int g = f - 1; g >= 0; g--)
-                if (((draw_encs >> (g + 1)) & (draw_encs >> (f + 1)) & 1u) &&
-                    wave_or(((rem_l >> (f + 1)) ^ (rem_l >> (g + 1))) & 1u) == 0u)
-                    rep[f] = rep[g];
-        }
-        const int32_t* order = p.place_order ? p.place_order + (size_t)blockIdx.x * A : nullptr;
-        for (int pass = 0; pass < 2; pass++) {
-            for (int k = 0; k < A; k++) {
-                const int a = order ? (int)uni(order[k]) : k;
-                const int ir = rl(L.init_r, a);
-                const bool has_ip = ir >= 0;
-                if ((pass == 0) != has_ip) continue;
-                const int aenc = rl(L.enc, a);
-                const uint32_t aov = rl(L.ov, a);
-                int cell;
-                if (has_ip) {
-                    cell = to_free(ir * p.W + rl(L.init_c, a));
-                    // Grid.place -> query (grid.py:81-129), asserted by the reference
-                    const bool blocks = valid && L.in_grid && cell_l == cell && !((aov >> L.enc) & 1u);
-                    if (__ballot(blocks)) { err |= GW_ERR_INIT_POSITION; return false; }
-                } else {
-                    int fa = 0;
-#pragma unroll
-                    for (int f = 1; f < SORT_LISTS; f++)
-                        if (aenc == f + 1) fa = rep[f];
-                    int Ra = R[0], ma = m[0];
-#pragma unroll
-                    for (int f = 1; f < SORT_LISTS; f++)
-                        if (fa == f) { Ra = R[f]; ma = m[f]; }
-                    const int n = NF - ma;
-                    if (n <= 0) { err |= GW_ERR_NO_CELL; return false; }
-                    const int idx = (int)rng.interval((uint32_t)(n - 1));   // np.random.choice(list, 1)
-                    cell = idx + __popcll(__ballot(l < ma && Ra - l <= idx));
-                    CHECK(cell >= 0 && cell < NF, 7, cell, a);
-                }
-                // _update_available_positions (state.py:126-141)
-                const uint32_t rem = (p.no_overlap_at_reset ? all_encs : (all_encs & ~aov)) & draw_encs;
-#pragma unroll
-                for (int f = 0; f < SORT_LISTS; f++) {
-                    if (!((rem >> (f + 1)) & 1u) || rep[f] != f) continue;
-                    if (__ballot(R[f] == cell)) continue;             // already removed
-                    const int pos = __popcll(__ballot(R[f] < cell));
-                    const int sh = (int)dpp<0x138>((uint32_t)R[f], (uint32_t)R[f]);   // wave_shr:1
-                    R[f] = l < pos ? R[f] : (l == pos ? cell : sh);
-                    m[f]++;
-                }
-                if (l == a) { cell_l = cell; L.in_grid = true; L.seq = ctr; }
-                ctr++;
-            }
-        }
-        if (L.in_grid) { const int gc = to_cell(cell_l); L.r = gc / p.W; L.c = gc % p.W; }
-        return true;
-    };
-
     auto place = [&]() -> bool {
-        if (GW_SORTED_PLACE && p.max_enc <= SORT_LISTS) return position_reset_sorted();
         // the Jacobi form solves lane order only: a shuffled order runs serially
         if (p.place_order) return position_reset_lanes();
         const int r = position_reset_jacobi();
@@ -2409,10 +2323,9 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     // runs several steps: nearly every env of a fragment draws beyond its
     // cached block (crowded cells, placements), and a load on demand puts a
     // memory round trip on that env's chain
-#ifndef GW_KEY_PREFETCH
-#define GW_KEY_PREFETCH 1
-#endif
-    const bool kpre = GW_KEY_PREFETCH == 2 || (GW_KEY_PREFETCH == 1 && p.nsteps > 1);
+    // (also for single-step launches: measured 0.5-1 % slower, the envs that
+    // draw nothing pay the load; profiles/r04/ab_closed_loop.jsonl)
+    const bool kpre = p.nsteps > 1;
     uint4 kq0 = {}, kq1 = {}, kq2 = {};
     if (kpre) {
         const uint4* ks = (const uint4*)(p.mt + (size_t)e * GW_MT_STRIDE);
