@@ -1,0 +1,99 @@
+"""Register and scratch budgets of the benched kernels, read from the built
+library's gfx950 code objects (AMDGPU metadata notes; CPU only).
+
+The launch shapes depend on them:
+  * step_kernel<7, 1> (the headline) holds 4 one-wave envs per SIMD, so all
+    4096 envs are resident at once on 1024 SIMDs: <= 128 VGPRs;
+  * wg_step_kernel<7> (config 4) fits 3 workgroups per CU only at <= 168
+    unified registers (512 / 3 in granules of 8): at 2 per CU the 1024-env
+    launch runs as two rounds (measured 3.83 vs 3.94 ms, 22.5 vs 30.5 ms at
+    8192 envs, profiles/r04/ab_wg_fresh_params_*.jsonl);
+  * no benched step kernel touches scratch: every scratch-using build of the
+    workgroup kernel measured slower (profiles/r04/ab_wg_min_waves.txt).
+"""
+import os
+import re
+import struct
+
+import pytest
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   'abmarl_amd', '_build', 'libgw_engine.so')
+
+
+def _sections(d):
+    shoff = struct.unpack_from('<Q', d, 0x28)[0]
+    ent, num, stri = struct.unpack_from('<HHH', d, 0x3A)
+    secs = [struct.unpack_from('<IIQQQQIIQQ', d, shoff + i * ent) for i in range(num)]
+    so = secs[stri][4]
+    return {d[so + s[0]:d.index(b'\0', so + s[0])].decode(): s for s in secs}
+
+
+def kernel_metadata(path=LIB):
+    """{kernel symbol: metadata map} of every gfx950 code object in the
+    library's offload bundles (.hip_fatbin)."""
+    import msgpack
+    data = open(path, 'rb').read()
+    fb = _sections(data)['.hip_fatbin']
+    blob = data[fb[4]:fb[4] + fb[5]]
+    out = {}
+    for st in [m.start() for m in re.finditer(b'__CLANG_OFFLOAD_BUNDLE__', blob)]:
+        n = struct.unpack_from('<Q', blob, st + 24)[0]
+        p = st + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from('<QQQ', blob, p)
+            p += 24
+            triple = blob[p:p + tl].decode()
+            p += tl
+            if 'gfx950' not in triple:
+                continue
+            co = blob[st + off:st + off + size]
+            ns = _sections(co)['.note']
+            note, q = co[ns[4]:ns[4] + ns[5]], 0
+            while q < len(note):
+                nsz, dsz, typ = struct.unpack_from('<III', note, q)
+                q += 12
+                name = note[q:q + nsz]
+                q += (nsz + 3) & ~3
+                desc = note[q:q + dsz]
+                q += (dsz + 3) & ~3
+                if name.startswith(b'AMDGPU') and typ == 32:
+                    for k in msgpack.unpackb(desc, raw=False)['amdhsa.kernels']:
+                        out[k['.name']] = k
+    return out
+
+
+@pytest.fixture(scope='module')
+def md():
+    if not os.path.exists(LIB):
+        pytest.skip('engine library not built')
+    pytest.importorskip('msgpack')
+    return kernel_metadata()
+
+
+def _get(md, pattern):
+    hits = [v for k, v in md.items() if re.search(pattern, k)]
+    assert len(hits) == 1, (pattern, len(hits))
+    return hits[0]
+
+
+def _granules(v):
+    return (v + 7) // 8 * 8
+
+
+def test_headline_kernel_four_envs_per_simd(md):
+    k = _get(md, r'11step_kernelILi7ELi1E')
+    assert _granules(k['.vgpr_count']) <= 128, k['.vgpr_count']
+    assert k['.private_segment_fixed_size'] == 0
+
+
+def test_workgroup_kernel_three_per_cu(md):
+    k = _get(md, r'14wg_step_kernelILi7E')
+    assert _granules(k['.vgpr_count']) <= 512 // 3, k['.vgpr_count']
+    assert k['.private_segment_fixed_size'] == 0
+
+
+@pytest.mark.parametrize('pattern', [r'10pac_kernelILi3E', r'10pac_kernelILi4E',
+                                     r'16lane_step_kernelILi5ELi10E'])
+def test_benched_kernels_without_scratch(md, pattern):
+    assert _get(md, pattern)['.private_segment_fixed_size'] == 0
