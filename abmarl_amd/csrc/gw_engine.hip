@@ -3798,8 +3798,11 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         // pac_carve: cval | pb | clist | cp | penc
         const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
                           align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS;
-        const size_t wb = work_bytes(HW, A, g->S, max_enc);
-        if (pw > wb) g->smem_step += pw - wb;
+        // the Pacman program never places by draws (every entity starts at its
+        // initial position): no placement scratch in its work area, so more
+        // envs share a CU (8.2 KB -> 5.4 KB per env at pacman.txt's 21x21)
+        g->smem_step = align16(GW_MT_N * 4) + align16((size_t)p.tbl_rows * p.pitch) +
+                       align16((size_t)((HW + 3) / 4) * 4) + pw;
     }
     g->smem_reset = g->smem_step;
     if (wg) {

@@ -8,8 +8,9 @@ The launch shapes depend on them:
     unified registers (512 / 3 in granules of 8): at 2 per CU the 1024-env
     launch runs as two rounds (measured 3.83 vs 3.94 ms, 22.5 vs 30.5 ms at
     8192 envs, profiles/r04/ab_wg_fresh_params_*.jsonl);
-  * no benched step kernel touches scratch: every scratch-using build of the
-    workgroup kernel measured slower (profiles/r04/ab_wg_min_waves.txt).
+  * the workgroup and headline kernels touch no scratch: every scratch-using
+    build of the workgroup kernel measured slower (profiles/r04/ab_wg_min_waves.txt);
+  * pac_kernel runs 6 waves per SIMD (config 5: 16384 envs).
 """
 import os
 import re
@@ -93,7 +94,14 @@ def test_workgroup_kernel_three_per_cu(md):
     assert k['.private_segment_fixed_size'] == 0
 
 
-@pytest.mark.parametrize('pattern', [r'10pac_kernelILi3E', r'10pac_kernelILi4E',
-                                     r'16lane_step_kernelILi5ELi10E'])
-def test_benched_kernels_without_scratch(md, pattern):
-    assert _get(md, pattern)['.private_segment_fixed_size'] == 0
+def test_pacman_kernel_six_per_simd(md):
+    """pac_kernel's step protocols at 6 waves per SIMD (launch bound; 16 B of
+    spill measured faster than 5 waves without, profiles/r04/ab_pac_waves*)."""
+    for pattern in (r'10pac_kernelILi3E', r'10pac_kernelILi4E'):
+        k = _get(md, pattern)
+        assert _granules(k['.vgpr_count']) <= 512 // 6, k['.vgpr_count']
+        assert k['.private_segment_fixed_size'] <= 16
+
+
+def test_maze_kernel_without_scratch(md):
+    assert _get(md, r'16lane_step_kernelILi5ELi10E')['.private_segment_fixed_size'] == 0
