@@ -163,6 +163,7 @@ struct Params {
     int32_t n_passive, pwords;             // passive entities (food), bit words per env
     const int16_t* passive_cell;           // [n_passive] cell
     const int16_t* cell_passive;           // [HW] passive index, -1 = none
+    const uint32_t* passive_cnt;           // [ceil(HW/4)] packed u8: passive entities per cell
     const int8_t* passive_enc;             // [n_passive]
     uint32_t* pbits;                       // [E][pwords] passive present
     double* racc;                          // [E][A] SmartGWS.rewards accumulators
@@ -3797,7 +3798,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     if (pac) {
         // pac_carve: cval | pb | clist | cp | penc
         const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
-                          align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS;
+                          align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS + 64 * PAC_MAX_PWORDS;
         // the Pacman program never places by draws (every entity starts at its
         // initial position): no placement scratch in its work area, so more
         // envs share a CU (8.2 KB -> 5.4 KB per env at pacman.txt's 21x21)
@@ -3852,21 +3853,33 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             if ((hs[l].kind & GW_K_OBSERVING) && (hs[l].kind & GW_K_ACTING)) p.agent_lanes |= 1ull << l;
         p.n_passive = (int)passive.size();
         p.pwords = (p.n_passive + 31) / 32;
-        std::vector<int16_t> pc(p.n_passive + HW, (int16_t)-1);
-        std::vector<int8_t> pe(p.n_passive > 0 ? p.n_passive : 1, 0);
+        // the program's constant tables, each starting on 16 bytes and padded
+        // to 16 (the kernel copies them to LDS with one 16-byte load per lane):
+        // passive cells [n] i16 | cell -> passive [HW] i16 | per-cell counts
+        // [ceil(HW/4)] u32; passive encodings [n] i8 (own allocation)
+        const size_t n8 = ((size_t)p.n_passive + 7) & ~(size_t)7;        // i16s, 16 B
+        const size_t hw8 = ((size_t)HW + 7) & ~(size_t)7;
+        const size_t cw = (((size_t)HW + 3) / 4 + 3) & ~(size_t)3;       // u32s, 16 B
+        std::vector<int16_t> pc(n8 + hw8 + 2 * cw, (int16_t)-1);
+        std::vector<uint32_t> cnt(cw, 0u);
+        std::vector<int8_t> pe((p.n_passive + 15) & ~15, 0);
+        if (pe.empty()) pe.resize(16, 0);
         for (int k = 0; k < p.n_passive; k++) {
             const gw_agent_spec& s = cfg->agents[passive[k]];
             const int cell = s.init_row * cfg->cols + s.init_col;
             pc[k] = (int16_t)cell;
-            pc[p.n_passive + cell] = (int16_t)k;
+            pc[n8 + cell] = (int16_t)k;
+            cnt[cell >> 2] += 1u << (8 * (cell & 3));
             pe[k] = (int8_t)s.encoding;
         }
+        memcpy(pc.data() + n8 + hw8, cnt.data(), cw * 4);
         HIPCHK(hipMalloc(&g->d_passive, pc.size() * 2));
         HIPCHK(hipMemcpy(g->d_passive, pc.data(), pc.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMalloc(&g->d_passive_enc, pe.size()));
         HIPCHK(hipMemcpy(g->d_passive_enc, pe.data(), pe.size(), hipMemcpyHostToDevice));
         p.passive_cell = g->d_passive;
-        p.cell_passive = g->d_passive + p.n_passive;
+        p.cell_passive = g->d_passive + n8;
+        p.passive_cnt = (const uint32_t*)(g->d_passive + n8 + hw8);
         p.passive_enc = g->d_passive_enc;
         const size_t pwn = (size_t)n_envs * (p.pwords > 0 ? p.pwords : 1);
         HIPCHK(hipMalloc(&p.pbits, pwn * 4));
