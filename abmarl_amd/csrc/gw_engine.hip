@@ -2502,7 +2502,12 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // isolation: no other mover targets my source or target, none leaves my target
                 const int HW = p.H * p.W;
                 const int nw = (HW + 3) / 4;
-                for (int i = l; i < nw; i += WAVE) { sm.tcnt[i] = 0u; sm.scnt[i] = 0u; }
+                {
+                    // 16-byte stores (both arrays start on 16 bytes, padded)
+                    const int nw4 = (nw + 3) >> 2;
+                    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+                    for (int i = l; i < nw4; i += WAVE) { ((uint4*)sm.tcnt)[i] = z; ((uint4*)sm.scnt)[i] = z; }
+                }
                 wave_sync();
                 const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
                 if (real) {
