@@ -95,12 +95,12 @@ def test_workgroup_kernel_three_per_cu(md):
 
 
 def test_pacman_kernel_six_per_simd(md):
-    """pac_kernel's step protocols at 6 waves per SIMD (launch bound; 16 B of
-    spill measured faster than 5 waves without, profiles/r04/ab_pac_waves*)."""
+    """pac_kernel's step protocols at 6 waves per SIMD (launch bound; up to 32 B
+    of spill measured faster than 5 waves without, profiles/r04/ab_pac_waves*)."""
     for pattern in (r'10pac_kernelILi3E', r'10pac_kernelILi4E'):
         k = _get(md, pattern)
         assert _granules(k['.vgpr_count']) <= 512 // 6, k['.vgpr_count']
-        assert k['.private_segment_fixed_size'] <= 16
+        assert k['.private_segment_fixed_size'] <= 32
 
 
 def test_maze_kernel_without_scratch(md):
