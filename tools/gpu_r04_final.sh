@@ -14,4 +14,7 @@ else
   timeout -k 10 560 bash tools/prof_headline.sh r04z > gpurun_out/ph_r04z.log 2>&1 || { echo PROF FAIL; tail -20 gpurun_out/ph_r04z.log; exit 1; }
   timeout -k 10 560 bash tools/prof_headline.sh r04zrtt rtt > gpurun_out/ph_r04zrtt.log 2>&1 || { echo PROF RTT FAIL; tail -20 gpurun_out/ph_r04zrtt.log; exit 1; }
   grep -h "timed launch\|HBM traffic\|waiting" gpurun_out/ph_r04z/profiles/*summary.md gpurun_out/ph_r04zrtt/profiles/*summary.md
+  if [ -f abmarl_amd/_build/libgw_engine_wunroll.so ]; then
+    bash tools/ab_rtt.sh abmarl_amd/_build/libgw_engine.so abmarl_amd/_build/libgw_engine_wunroll.so || exit 1
+  fi
 fi
