@@ -3801,8 +3801,8 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.pair_cap = (int)((work_bytes(HW, A, Sst, max_enc) - (size_t)A * Sst * ((Sst + 3) & ~3)) / 2);
     g->smem_step = smem_bytes(HW, A, Sst, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
-        // pac_carve: cval | pb | crowded rows [4][64] | cp | penc | passive cells
-        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * 4 * WAVE +
+        // pac_carve: cval | pb | clist | cp | penc
+        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
                           align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS + 64 * PAC_MAX_PWORDS;
         // the Pacman program never places by draws (every entity starts at its
         // initial position): no placement scratch in its work area, so more
