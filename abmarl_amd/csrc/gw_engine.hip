@@ -2402,13 +2402,6 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         // first observation, reward 0, done = not an Agent, no __all__
         const bool next_reset = p.autoreset == 2 && (prev_all || (p.horizon > 0 && steps >= p.horizon));
         bool reset_now = next_reset;
-#ifndef GW_RESET_PRIO1
-#define GW_RESET_PRIO1 1
-#endif
-        // a single-step launch lasts as long as its resetting envs (placement,
-        // health draws, first observation: several times a step): they issue
-        // first on their SIMD
-        if (GW_RESET_PRIO1 && p.nsteps == 1 && next_reset) set_prio(3);
         if (!next_reset) {
             if (ctr >= SEQ_RENORM) renorm_seq(p, L, ctr);
             const bool acting = valid && L.live && ak >= 0;
