@@ -667,6 +667,7 @@ struct Smem {
 // (sized so that the TeamBattle 32x32 env fits 10 KiB of LDS: 16 one-wave
 // envs per CU, all 4096 resident at once on 256 CUs)
 constexpr int JAC_WB = 160;
+static_assert(JAC_WB < GW_MT_N - 397, "placement words past the twist come from the untwisted key");
 constexpr int JAC_OFF_W = 0;
 constexpr int JAC_OFF_PUB = JAC_OFF_W + 4 * JAC_WB;
 constexpr int JAC_OFF_CP = JAC_OFF_PUB + 4 * 64;
@@ -1975,7 +1976,6 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint32_t* cpa = (uint32_t*)(sm.stage + JAC_OFF_CP);
         uint2* sb = (uint2*)(sm.stage + JAC_OFF_SB);
         uint2* tb = (uint2*)(sm.stage + JAC_OFF_T);
-        uint32_t* key2 = (uint32_t*)(sm.stage + JAC_OFF_KEY2);
         uint32_t* hist = sm.cnt;   // rebuilt by build_tables afterwards
         const int nw = (NF + 3) >> 2;
         int chs = 4;               // chunk of 1 << chs cells per lane (>= 16)
@@ -2026,11 +2026,18 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                 if (k < GW_MT_N) wbuf[t] = temper(rng.key[k]);
             }
             if (crosses) {
-                for (int i = l; i < GW_MT_N; i += WAVE) key2[i] = rng.key[i];
-                mt_twist(key2);
+                // word j < 227 of the next key needs only the current one
+                // (mt19937's twist rewrites key[j] from key[j], key[j + 1]
+                // and key[j + 397], none rewritten yet for j < 227): the
+                // words past the twist without twisting (JAC_WB < 227).
+                // Indices clamped, every read in range for every lane.
                 for (int t = l; t < JAC_WB; t += WAVE) {
-                    const int k = pos0 + t - GW_MT_N;
-                    if (k >= 0) wbuf[t] = temper(key2[k]);
+                    const int j = pos0 + t - GW_MT_N;
+                    const int jj = j < 0 ? 0 : j;
+                    const uint32_t k0 = rng.key[CIDX(jj, GW_MT_N, 21)], k1 = rng.key[CIDX(jj + 1, GW_MT_N, 21)];
+                    const uint32_t k397 = rng.key[CIDX(jj + 397, GW_MT_N, 21)];
+                    const uint32_t y = (k0 & 0x80000000u) | (k1 & 0x7fffffffu);
+                    if (j >= 0) wbuf[t] = temper(k397 ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
                 }
             }
             wave_sync();
@@ -2168,9 +2175,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         if (__ballot(rnd && n == 0)) return 2;   // the serial loop raises at the right point
         const int total = (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
         const int np = pos0 + total;
-        if (np > GW_MT_N) {   // the draws crossed the twist: the copy is the live key
-            for (int i = l; i < GW_MT_N; i += WAVE) rng.key[i] = key2[i];
-            wave_sync();
+        if (np > GW_MT_N) {   // the draws crossed the twist: twist the live key
+            mt_twist(rng.key);
             rng.pos = np - GW_MT_N;
             rng.dirty = true;
         } else {
