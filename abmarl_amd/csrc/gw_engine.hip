@@ -2176,7 +2176,14 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const int total = (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
         const int np = pos0 + total;
         if (np > GW_MT_N) {   // the draws crossed the twist: twist the live key
+            // (the out-of-line twist every draw site uses, LDS-typed pointer;
+            // the inlined loop on rng.key faulted in reset_kernel<0>, whose
+            // state lives partly in scratch)
+#if GW_TWIST_CALL
+            mt_twist_call((__attribute__((address_space(3))) uint32_t*)rng.key);
+#else
             mt_twist(rng.key);
+#endif
             rng.pos = np - GW_MT_N;
             rng.dirty = true;
         } else {
