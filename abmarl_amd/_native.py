@@ -25,6 +25,9 @@ if os.environ.get('GW_ENGINE_STAMPS') == '1':
 
 def variant_lib(variant=None):
     v = VARIANT if variant is None else variant
+    # GW_ENGINE_LIB (diagnostic runs only) replaces the selected variant's library
+    if variant is None and os.environ.get('GW_ENGINE_LIB'):
+        return LIB
     return {'': LIB, 'stamps': LIB_STAMPS, 'checks': LIB_CHECKS}[v]
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('GW_OFFLOAD_ARCH', 'gfx950')

@@ -280,9 +280,6 @@ __device__ __forceinline__ void buf_store_i8x4(__amdgpu_buffer_rsrc_t rs, uint32
 // values -- and the 64-bit lane masks of every loop-invariant config test --
 // held live across the loop, which overflow the SGPR file and spill into
 // VGPR lanes (a v_writelane / v_readlane pair per reload, VALU work).
-#ifndef GW_FRESH_PARAMS
-#define GW_FRESH_PARAMS 1
-#endif
 struct Params;
 __device__ __forceinline__ const Params& kernel_params()
 {
@@ -424,47 +421,28 @@ __device__ __forceinline__ uint32_t temper(uint32_t y)
     return y;
 }
 
+// The MT19937 key always lives in LDS and is always addressed through an
+// LDS-typed (address space 3) pointer, so every access to it is a ds_*
+// instruction whatever the surrounding code does with the pointer.
+//
+// Why it matters (the round-4 fault, DESIGN §4 "MT19937 key addressing"):
+// in the generic-window instantiations (S = 0: observe_big is an out-of-line
+// call taking the Rng / Smem by reference, so they live in scratch) a plain
+// `uint32_t*` key is a generic pointer.  LLVM then lowers the twist's
+// key[i], key[i + 1] pair to ONE flat_load_dwordx2 at key + 4i: legal for
+// FLAT (dword alignment suffices for global memory), but for odd i the
+// address is 4 mod 8 inside the LDS aperture, and a 64-bit LDS access off
+// its natural alignment is a memory violation (the same pair through an
+// LDS-typed pointer is a ds_read2_b32, two dword accesses).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
 // mt19937.c mt19937_gen, lane-parallel in chunks of 64 (every write's
 // dependency i-227 is >= 3 chunks back; i+1 is read before any lane writes)
-__device__ __forceinline__ void mt_twist(uint32_t* key)
+__device__ __forceinline__ void mt_twist(lds_u32* key)
 {
     const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
     const int l = lane_id();
     wave_sync();
-    for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
-        int i = b + l;
-        uint32_t nv = 0;
-        if (i < GW_MT_N - 1) {
-            uint32_t y = (key[i] & UP) | (key[i + 1] & LO);
-            int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
-            nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
-        }
-        wave_sync();
-        if (i < GW_MT_N - 1) key[i] = nv;
-        wave_sync();
-    }
-    {
-        uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
-        uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
-        wave_sync();
-        if (l == 0) key[GW_MT_N - 1] = nv;
-        wave_sync();
-    }
-}
-
-// The twist of a draw that crosses the key's end, as ONE out-of-line copy:
-// Rng::next is inlined at every draw site, and a full twist loop at each of
-// them made the kernels several times larger than the instruction cache.
-// The key pointer is an LDS (address space 3) one, so the callee's accesses
-// stay ds_* operations.
-#ifndef GW_TWIST_CALL
-#define GW_TWIST_CALL 1
-#endif
-__device__ __noinline__ void mt_twist_call(__attribute__((address_space(3))) uint32_t* key)
-{
-    const uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MA = 0x9908b0dfu;
-    const int l = lane_id();
-    __builtin_amdgcn_wave_barrier();
     for (int b = 0; b < GW_MT_N - 1; b += WAVE) {
         const int i = b + l;
         uint32_t nv = 0;
@@ -473,24 +451,21 @@ __device__ __noinline__ void mt_twist_call(__attribute__((address_space(3))) uin
             int j = i + 397; if (j >= GW_MT_N) j -= GW_MT_N;
             nv = key[j] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
         if (i < GW_MT_N - 1) key[i] = nv;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
     }
     const uint32_t y = (key[GW_MT_N - 1] & UP) | (key[0] & LO);
     const uint32_t nv = key[396] ^ (y >> 1) ^ ((y & 1u) ? MA : 0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
     if (l == 0) key[GW_MT_N - 1] = nv;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
 }
+
+// The twist of a draw that crosses the key's end, as ONE out-of-line copy:
+// Rng::next is inlined at every draw site, and a full twist loop at each of
+// them made the kernels several times larger than the instruction cache.
+__device__ __noinline__ void mt_twist_call(lds_u32* key) { mt_twist(key); }
 
 // numpy legacy RandomState (mt19937.c).  The 624-word key stays in HBM until
 // a draw needs it (a word outside the cached block, a twist, a reset); it is
@@ -498,7 +473,7 @@ __device__ __noinline__ void mt_twist_call(__attribute__((address_space(3))) uin
 // kept per env in HBM (mt[MT_CACHE..]) and in a register, one word per lane,
 // so a draw is one v_readlane and most launches never read the key.
 struct Rng {
-    uint32_t* key;          // LDS [624] (valid once loaded)
+    lds_u32* key;           // LDS [624] (valid once loaded)
     const uint32_t* gkey;   // this env's key in HBM
     uint32_t cache;         // tempered key[base + lane] (lane < ccount)
     int pos;                // next index (wave-uniform)
@@ -526,11 +501,7 @@ struct Rng {
     __device__ __forceinline__ void twist()
     {
         ensure_key();
-#if GW_TWIST_CALL
-        mt_twist_call((__attribute__((address_space(3))) uint32_t*)key);
-#else
-        mt_twist(key);
-#endif
+        mt_twist_call(key);
         pos = 0;
         base = -1;
         dirty = true;
@@ -653,7 +624,7 @@ __device__ __forceinline__ void store_lane(const Params& p, int e, const Lane& L
 //   work union: { tcnt, scnt [2][ceil(HW/4)] u32 (move isolation)
 //               | stage [A*SS] i8 (observations) }
 struct Smem {
-    uint32_t* key;
+    lds_u32* key;
     uint8_t* tbl;
     uint32_t* cnt;
     uint32_t* tcnt;
@@ -697,7 +668,7 @@ __device__ __forceinline__ Smem carve(char* base, const Params& p)
 {
     const int HW = p.H * p.W;
     Smem s;
-    s.key = (uint32_t*)base; base += align16(GW_MT_N * 4);
+    s.key = (lds_u32*)base; base += align16(GW_MT_N * 4);
     s.tbl = (uint8_t*)base; base += align16((size_t)p.tbl_rows * p.pitch);
     s.cnt = (uint32_t*)base; base += align16((size_t)((HW + 3) / 4) * 4);
     s.tcnt = (uint32_t*)base;
@@ -1258,7 +1229,7 @@ __device__ __forceinline__ void observe_fixed(const Params& p, int e, Smem& sm, 
 // and for a crowded cell np.random.choice over the occupants' encodings in
 // insertion (seq) order without the observer when observe_self is off --
 // the draws in (observer, row, col) order as in the reference's loops.
-__device__ __noinline__ void observe_big(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, int32_t* obs)
+__device__ __forceinline__ void observe_big(const Params& p, int e, Smem& sm, Rng& rng, Lane& L, int32_t* obs)
 {
     const int S = p.obs_side, R = S / 2, SS = S * S;
     const int l = lane_id(), A = p.A;
@@ -2176,14 +2147,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const int total = (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
         const int np = pos0 + total;
         if (np > GW_MT_N) {   // the draws crossed the twist: twist the live key
-            // (the out-of-line twist every draw site uses, LDS-typed pointer;
-            // the inlined loop on rng.key faulted in reset_kernel<0>, whose
-            // state lives partly in scratch)
-#if GW_TWIST_CALL
-            mt_twist_call((__attribute__((address_space(3))) uint32_t*)rng.key);
-#else
-            mt_twist(rng.key);
-#endif
+            mt_twist_call(rng.key);
             rng.pos = np - GW_MT_N;
             rng.dirty = true;
         } else {
@@ -2374,9 +2338,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     // the first step that needs them (a reset adds its own)
     bool lanes_in = false, need_tmpl = false;
     for (int t = 0; t < p.nsteps; t++) {
-#if GW_FRESH_PARAMS
         const Params& p = kernel_params();
-#endif
         // issue priority (gw_rollout): the four envs of a SIMD start together,
         // and VALU issue goes by priority, then age, so a heavy young wave
         // would trail the others and end the launch alone.  Remaining-work

@@ -201,6 +201,21 @@ def test_blocking_configs(oracle_mod, kw):
     _run(oracle_mod, cc, E=512, T=150, horizon=50, seed_run=7, key=9)
 
 
+def test_generic_window_resets_cross_the_twist(oracle_mod):
+    """The generic-window kernels (view 8: window side 17 > 15, so
+    reset_kernel<0> / step_kernel<0, 0>, whose Rng and Smem live in scratch
+    behind the out-of-line observe_big) on 64 random-health fighters: every
+    reset draws 128 health words and the placement's, so a third of the
+    resets cross the MT19937 twist in the health reset and in the placement
+    -- the sites that read the key through a generic pointer (FLAT) until
+    round 5 (DESIGN §4 "MT19937 key addressing")."""
+    cc = team_battle(rows=20, cols=20, n_agents=64, n_teams=2,
+                     agent=dict(move_range=1, attack_range=1, attack_strength=1, attack_accuracy=1,
+                                view_range=8))
+    assert cc.obs_side == 17            # > 2 * GW_FIXED_RANGE + 1: the generic window path
+    _run(oracle_mod, cc, E=256, T=120, horizon=25, seed_run=5, key=31, check_every=3)
+
+
 def test_next_step_autoreset_4096_envs(oracle_mod):
     """gw_step_autoreset_next on the headline config: envs whose episode ended
     in the previous call are reset (reward 0, done only for non-Agents, actions

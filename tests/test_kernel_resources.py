@@ -30,14 +30,13 @@ def _sections(d):
     return {d[so + s[0]:d.index(b'\0', so + s[0])].decode(): s for s in secs}
 
 
-def kernel_metadata(path=LIB):
-    """{kernel symbol: metadata map} of every gfx950 code object in the
-    library's offload bundles (.hip_fatbin)."""
-    import msgpack
+def code_objects(path=LIB):
+    """The gfx950 code objects (ELF images) in the library's offload bundles
+    (.hip_fatbin)."""
     data = open(path, 'rb').read()
     fb = _sections(data)['.hip_fatbin']
     blob = data[fb[4]:fb[4] + fb[5]]
-    out = {}
+    out = []
     for st in [m.start() for m in re.finditer(b'__CLANG_OFFLOAD_BUNDLE__', blob)]:
         n = struct.unpack_from('<Q', blob, st + 24)[0]
         p = st + 32
@@ -46,21 +45,29 @@ def kernel_metadata(path=LIB):
             p += 24
             triple = blob[p:p + tl].decode()
             p += tl
-            if 'gfx950' not in triple:
-                continue
-            co = blob[st + off:st + off + size]
-            ns = _sections(co)['.note']
-            note, q = co[ns[4]:ns[4] + ns[5]], 0
-            while q < len(note):
-                nsz, dsz, typ = struct.unpack_from('<III', note, q)
-                q += 12
-                name = note[q:q + nsz]
-                q += (nsz + 3) & ~3
-                desc = note[q:q + dsz]
-                q += (dsz + 3) & ~3
-                if name.startswith(b'AMDGPU') and typ == 32:
-                    for k in msgpack.unpackb(desc, raw=False)['amdhsa.kernels']:
-                        out[k['.name']] = k
+            if 'gfx950' in triple:
+                out.append(blob[st + off:st + off + size])
+    return out
+
+
+def kernel_metadata(path=LIB):
+    """{kernel symbol: metadata map} of every gfx950 code object in the
+    library's offload bundles (.hip_fatbin)."""
+    import msgpack
+    out = {}
+    for co in code_objects(path):
+        ns = _sections(co)['.note']
+        note, q = co[ns[4]:ns[4] + ns[5]], 0
+        while q < len(note):
+            nsz, dsz, typ = struct.unpack_from('<III', note, q)
+            q += 12
+            name = note[q:q + nsz]
+            q += (nsz + 3) & ~3
+            desc = note[q:q + dsz]
+            q += (dsz + 3) & ~3
+            if name.startswith(b'AMDGPU') and typ == 32:
+                for k in msgpack.unpackb(desc, raw=False)['amdhsa.kernels']:
+                    out[k['.name']] = k
     return out
 
 
@@ -105,3 +112,53 @@ def test_pacman_kernel_six_per_simd(md):
 
 def test_maze_kernel_without_scratch(md):
     assert _get(md, r'16lane_step_kernelILi5ELi10E')['.private_segment_fixed_size'] == 0
+
+
+OBJDUMP = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+
+
+def twist_memory_ops(path):
+    """{function: set of memory opcodes} of every MT19937 twist block in the
+    library's gfx950 code: the 0x9908b0df mask of mt19937's twist and the 25
+    instructions before it, where the key words are read."""
+    import subprocess
+    import tempfile
+    found = {}
+    for co in code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix='.co') as f:
+            f.write(co)
+            f.flush()
+            txt = subprocess.run([OBJDUMP, '-d', '--mcpu=gfx950', f.name], check=True,
+                                 capture_output=True, text=True).stdout.split('\n')
+        fn = None
+        for i, ln in enumerate(txt):
+            m = re.match(r'^[0-9a-f]+ <(.+)>:', ln)
+            if m:
+                fn = m.group(1)
+            elif '0x9908b0df' in ln:
+                ops = {x.split()[0] for x in txt[max(0, i - 25):i]
+                       if x.strip().startswith(('flat_', 'ds_', 'global_', 'scratch_', 'buffer_'))
+                       for x in [x.strip()]}
+                found.setdefault(fn, set()).update(ops)
+    return found
+
+
+@pytest.mark.parametrize('variant', ['', 'checks'])
+def test_mt_key_never_read_through_flat(variant):
+    """Every MT19937 twist in every kernel reads the key with ds_* operations:
+    the key pointer is LDS-typed (lds_u32) everywhere.  A generic key pointer
+    in a scratch-resident Rng (the generic-window kernels, the checks build)
+    made LLVM read the key[i] / key[i + 1] pair as ONE flat_load_dwordx2 at
+    key + 4i -- a 64-bit LDS access off its natural alignment for odd i, the
+    round-4 memory aperture violation (DESIGN §4 "MT19937 key addressing")."""
+    from abmarl_amd import _native
+    path = _native.variant_lib(variant)
+    if not os.path.exists(path):
+        pytest.skip(f'{os.path.basename(path)} not built')
+    if not os.path.exists(OBJDUMP):
+        pytest.skip('llvm-objdump missing')
+    ops = twist_memory_ops(path)
+    assert ops, 'no twist found in the library'
+    bad = {fn: sorted(o) for fn, o in ops.items() if any(x.startswith('flat_') for x in o)}
+    assert not bad, bad
+    assert all(any(x.startswith('ds_') for x in o) for o in ops.values()), ops
