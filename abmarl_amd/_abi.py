@@ -28,6 +28,7 @@ GW_ERR_INIT_POSITION = 2
 GW_ERR_DOUBLE_REMOVE = 4
 GW_ERR_TUNNEL_PLACE = 8
 GW_ERR_NOT_IN_GRID = 16
+GW_ERR_VALUE_ERROR = 32
 
 GW_OP_POSITION_RESET = 1
 GW_OP_HEALTH_RESET = 2
@@ -135,6 +136,7 @@ class Config(C.Structure):
         ("all_lanes", C.c_int32),
         ("env_per_lane", C.c_int32),
         ("component_api", C.c_int32),
+        ("attack_array_as_list", C.c_int32),
     ]
 
 

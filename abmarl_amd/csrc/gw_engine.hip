@@ -131,6 +131,7 @@ struct Params {
     // config
     int32_t E, A, H, W, max_enc, sim_kind, nav, target;
     int32_t observe_self, stacked, no_overlap_at_reset, state_order;
+    int32_t arr_as_list;                   // gw_config.attack_array_as_list
     uint32_t done_kind;
     int32_t pad, pitch, tbl_rows;          // padded byte table geometry
     int32_t pair_cap;                      // crowded (observer, cell) pairs that fit after the obs stage
@@ -1363,12 +1364,14 @@ __device__ __forceinline__ bool attack_precheck(const Params& p, const Smem& sm,
 // for AmmoAgent attacker a (uniform): more attacked entries than ammo keeps
 // np.random.choice(attacked, ammo, replace=False) = entries permutation(n)[:ammo]
 // in that order (n - 1 interval draws, also for ammo 0); then ammo -= the
-// kept count.  list: lane t holds entry t.
-__device__ __forceinline__ void ammo_filter(Rng& rng, Lane& L, int a, int& nlist, int& list)
+// kept count.  list: lane t holds entry t.  Returns whether it chose (its
+// result is a list: .tolist(), actor.py:347-351).
+__device__ __forceinline__ bool ammo_filter(Rng& rng, Lane& L, int a, int& nlist, int& list)
 {
     const int l = lane_id();
     const int am = rl(L.ammo, a);
-    if (nlist > am) {
+    const bool chose = nlist > am;
+    if (chose) {
         int perm = l;
         for (int i = nlist - 1; i >= 1; i--) {
             const int j = (int)rng.interval((uint32_t)i);
@@ -1381,15 +1384,20 @@ __device__ __forceinline__ void ammo_filter(Rng& rng, Lane& L, int a, int& nlist
         nlist = am;
     }
     if (l == a) L.ammo = am - nlist;
+    return chose;
 }
 
 // BinaryAttackActor.process_action for attacker a with k attacks.
 // Returns status (attempted); list (register of lane t) = attacked lanes in
 // list order; applies damage and updates the cell table for kills.
+// *ndarray (optional): the attacked agents are the numpy array
+// _subset_attackables' np.random.choice returns (actor.py:412-414) and no
+// ammo filter turned them into a list (actor.py:347-351).
 template <bool PLAIN = false>
 __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, Lane& L, int a,
-                                           int k, int& nlist, int& list)
+                                           int k, int& nlist, int& list, bool* ndarray = nullptr)
 {
+    if (ndarray) *ndarray = false;
     const bool BL = !PLAIN && p.blockers, LB = !PLAIN && p.lane_blockers;
     const int l = lane_id();
     nlist = 0;
@@ -1464,6 +1472,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
             if (l == t) pick = idx;
         }
         nlist = k;
+        if (ndarray) *ndarray = true;
     } else {
         int perm = l;                                       // permutation(n)[:k]
         for (int i = n - 1; i >= 1; i--) {
@@ -1474,6 +1483,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         }
         pick = l < k ? perm : -1;
         nlist = k;
+        if (ndarray) *ndarray = true;
     }
     for (int t = 0; t < nlist; t++) {
         const int pr = rl(pick, t);
@@ -1482,7 +1492,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         const int lane_t = first_lane(tm);
         if (l == t) list = lane_t;
     }
-    if (!PLAIN && (akind & GW_K_AMMO)) ammo_filter(rng, L, a, nlist, list);
+    if (!PLAIN && (akind & GW_K_AMMO) && ammo_filter(rng, L, a, nlist, list) && ndarray) *ndarray = false;
     // apply damage in list order (actor.py:353-358)
     const double strength = rld(L.strength, a);
     for (int t = 0; t < nlist; t++) {
@@ -2385,7 +2395,9 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             if (!lanes_in) { build_tables(p, sm, L, false); lanes_in = true; }
             STAMP(1);
             L.reward = 0.0;
-            bool raised = false;                 // ReachTheTarget's double remove (KeyError)
+            // the step raised (GW_ERR_* bits): ReachTheTarget's double remove
+            // (KeyError), BinaryAttackActor's numpy array (ValueError)
+            uint32_t raised = 0u;
 
             // AllStepManager(randomize_action_input=True): the shuffled action
             // dict's order (the generic kernel only; TeamBattle, ReachTheTarget,
@@ -2441,7 +2453,12 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     }
                     if (!rlb(L.active, a)) return;                  // killed earlier this pass
                     int nlist, list;
-                    attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                    bool nd;
+                    attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list, &nd);
+                    // `not attacked_agents` (team_battle_example.py:41) on a numpy
+                    // array of 2 or more agents raises ValueError: the step stops
+                    // here, this attack applied
+                    if (nd && nlist >= 2 && !p.arr_as_list) { raised = GW_ERR_VALUE_ERROR; return; }
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
                         for (int t = 0; t < nlist; t++) {
@@ -2455,101 +2472,106 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 };
                 if (aord) {
                     // randomize_action_input: the action dict's order
-                    for (int k = 0; k < A; k++) {
+                    for (int k = 0; k < A && !raised; k++) {
                         const int a = uni(aord[k]);
                         if ((maybe_mask >> a) & 1ull) serial_attack(a, pend & __ballot(valid && my_rank < k));
                     }
                 } else {
-                    for (uint64_t it = maybe_mask; it; it &= it - 1) {
+                    for (uint64_t it = maybe_mask; it && !raised; it &= it - 1) {
                         const int a = first_lane(it);
                         serial_attack(a, pend & ((1ull << a) - 1ull));
                     }
                 }
                 if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
                 STAMP(2);
-                // ---- move pass (:50-55)
-                const bool mover = acting && L.active;
-                const bool can_move = mover && (L.kind & GW_K_MOVING);
-                const int nr = L.r + mr, nc = L.c + mc;
-                const bool inb = 0 <= nr && nr < p.H && 0 <= nc && nc < p.W;
-                const bool stay = nr == L.r && nc == L.c;
-                const bool real = can_move && inb && !stay;
-                // isolation: no other mover targets my source or target, none leaves my target
-                const int HW = p.H * p.W;
-                const int nw = (HW + 3) / 4;
-                {
-                    // 16-byte stores (both arrays start on 16 bytes, padded)
-                    const int nw4 = (nw + 3) >> 2;
-                    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-                    for (int i = l; i < nw4; i += WAVE) { ((uint4*)sm.tcnt)[i] = z; ((uint4*)sm.scnt)[i] = z; }
-                }
-                wave_sync();
-                const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
-                if (real) {
-                    atomicAdd(&sm.tcnt[cnt_word(p, tgt)], 1u << (8 * (tgt & 3)));
-                    atomicAdd(&sm.scnt[cnt_word(p, src)], 1u << (8 * (src & 3)));
-                }
-                wave_sync();
-                bool iso = false, iso_ok = false;
-                if (real && cnt_get(sm.tcnt, tgt) == 1 && cnt_get(sm.scnt, tgt) == 0 &&
-                    cnt_get(sm.tcnt, src) == 0) {
-                    const uint32_t b = sm.tbl[tbl_idx(p, nr, nc)];
-                    if (b != CELL_CROWD) { iso = true; iso_ok = (b == 0) || ((L.ov >> b) & 1u); }
-                }
-                const int pr = L.r, pc = L.c;
-                bool moved = false;
-                if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)my_rank; moved = true; }
-                bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
-        #ifdef GW_STAMPS
-                {
-                    const int nser = __popcll(__ballot(real && !iso)), nreal = __popcll(__ballot(real));
-                    if (l == 0 && p.stamps) { p.stamps[(size_t)e * GW_STAMP_STRIDE + 30] = nser; p.stamps[(size_t)e * GW_STAMP_STRIDE + 31] = nreal; }
-                }
-        #endif
-                STAMP(11);
-                const uint64_t ser = __ballot(real && !iso);
-                if (aord) {
-                    // randomize_action_input: movers in the action dict's
-                    // order, appended to their cells in that order
-                    for (int k = 0; k < A; k++) {
-                        const int a = uni(aord[k]);
-                        if (!((ser >> a) & 1ull)) continue;
-                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)k);
-                        if (l == a) { fail = !ok; moved = ok; }
+                if (!raised) {
+                    // ---- move pass (:50-55)
+                    const bool mover = acting && L.active;
+                    const bool can_move = mover && (L.kind & GW_K_MOVING);
+                    const int nr = L.r + mr, nc = L.c + mc;
+                    const bool inb = 0 <= nr && nr < p.H && 0 <= nc && nc < p.W;
+                    const bool stay = nr == L.r && nc == L.c;
+                    const bool real = can_move && inb && !stay;
+                    // isolation: no other mover targets my source or target, none leaves my target
+                    const int HW = p.H * p.W;
+                    const int nw = (HW + 3) / 4;
+                    {
+                        // 16-byte stores (both arrays start on 16 bytes, padded)
+                        const int nw4 = (nw + 3) >> 2;
+                        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+                        for (int i = l; i < nw4; i += WAVE) { ((uint4*)sm.tcnt)[i] = z; ((uint4*)sm.scnt)[i] = z; }
                     }
-                } else {
-                    for (uint64_t it = ser; it; it &= it - 1) {
-                        const int a = first_lane(it);
-                        const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
-                        if (l == a) { fail = !ok; moved = ok; }
+                    wave_sync();
+                    const int src = L.r * p.W + L.c, tgt = nr * p.W + nc;
+                    if (real) {
+                        atomicAdd(&sm.tcnt[cnt_word(p, tgt)], 1u << (8 * (tgt & 3)));
+                        atomicAdd(&sm.scnt[cnt_word(p, src)], 1u << (8 * (src & 3)));
                     }
+                    wave_sync();
+                    bool iso = false, iso_ok = false;
+                    if (real && cnt_get(sm.tcnt, tgt) == 1 && cnt_get(sm.scnt, tgt) == 0 &&
+                        cnt_get(sm.tcnt, src) == 0) {
+                        const uint32_t b = sm.tbl[tbl_idx(p, nr, nc)];
+                        if (b != CELL_CROWD) { iso = true; iso_ok = (b == 0) || ((L.ov >> b) & 1u); }
+                    }
+                    const int pr = L.r, pc = L.c;
+                    bool moved = false;
+                    if (iso && iso_ok) { L.r = nr; L.c = nc; L.seq = ctr + (uint32_t)my_rank; moved = true; }
+                    bool fail = (mover && !can_move) || (can_move && !inb) || (iso && !iso_ok);
+            #ifdef GW_STAMPS
+                    {
+                        const int nser = __popcll(__ballot(real && !iso)), nreal = __popcll(__ballot(real));
+                        if (l == 0 && p.stamps) { p.stamps[(size_t)e * GW_STAMP_STRIDE + 30] = nser; p.stamps[(size_t)e * GW_STAMP_STRIDE + 31] = nreal; }
+                    }
+            #endif
+                    STAMP(11);
+                    const uint64_t ser = __ballot(real && !iso);
+                    if (aord) {
+                        // randomize_action_input: movers in the action dict's
+                        // order, appended to their cells in that order
+                        for (int k = 0; k < A; k++) {
+                            const int a = uni(aord[k]);
+                            if (!((ser >> a) & 1ull)) continue;
+                            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)k);
+                            if (l == a) { fail = !ok; moved = ok; }
+                        }
+                    } else {
+                        for (uint64_t it = ser; it; it &= it - 1) {
+                            const int a = first_lane(it);
+                            const bool ok = move_one(p, L, a, rl(mr, a), rl(mc, a), ctr + (uint32_t)a);
+                            if (l == a) { fail = !ok; moved = ok; }
+                        }
+                    }
+                    if (fail) L.reward -= 0.1;
+                    ctr += (uint32_t)WAVE;
+                    // ---- entropy (:58-59)
+                    if (acting) L.reward -= 0.01;
+                    // cell table after the moves
+                    wave_sync();
+                    if (moved) {
+                        const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
+                        atomicSub(&sm.cnt[cnt_word(p, oc)], 1u << (8 * (oc & 3)));
+                        atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
+                        sm.tbl[tbl_idx(p, pr, pc)] = 0;
+                    }
+                    wave_sync();
+                    if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
+                    wave_sync();
                 }
-                if (fail) L.reward -= 0.1;
-                ctr += (uint32_t)WAVE;
-                // ---- entropy (:58-59)
-                if (acting) L.reward -= 0.01;
-                // cell table after the moves
-                wave_sync();
-                if (moved) {
-                    const int oc = pr * p.W + pc, ncl = L.r * p.W + L.c;
-                    atomicSub(&sm.cnt[cnt_word(p, oc)], 1u << (8 * (oc & 3)));
-                    atomicAdd(&sm.cnt[cnt_word(p, ncl)], 1u << (8 * (ncl & 3)));
-                    sm.tbl[tbl_idx(p, pr, pc)] = 0;
-                }
-                wave_sync();
-                if (L.in_grid) sm.tbl[tbl_idx(p, L.r, L.c)] = cell_byte(cnt_get(sm.cnt, L.r * p.W + L.c), L.enc);
-                wave_sync();
             } else if (sim_kind == GW_SIM_REACH_TARGET) {
                 // ---- attack pass (reach_the_target.py:96-108): every acting agent,
                 // dict order; only AttackingAgents attack (others return False, [])
                 const int32_t* act_e = act_t + (size_t)e * A * p.act_dim;
                 in_dict_order(__ballot(acting && (L.kind & GW_K_ATTACKING)), [&](int a, int) {
-                    if (!rlb(L.active, a)) return;
+                    if (raised || !rlb(L.active, a)) return;
                     int nlist, list;
+                    bool nd = false;
                     const bool status = p.attack_kind == GW_ATTACK_SELECTIVE
                         ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
-                        : attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list);
+                        : attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list, &nd);
                     if (!status) return;
+                    // `not attacked_agents` (reach_the_target.py:107) on a numpy array
+                    if (nd && nlist >= 2 && !p.arr_as_list) { raised = GW_ERR_VALUE_ERROR; return; }
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
                         for (int t = 0; t < nlist; t++) {
@@ -2580,7 +2602,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                             // further moves, no observation draws); the env needs a
                             // reset, which the auto-reset modes do as for an ended
                             // episode (all_done set; SAME_STEP resets it right away)
-                            raised = true;
+                            raised = GW_ERR_DOUBLE_REMOVE;
                             return;
                         }
                         if (l == a) {
@@ -2632,11 +2654,12 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             }
             STAMP(3);
             if (raised) {
-                // Grid.remove raised KeyError: the step stops here (no further
-                // moves, no observation draws, its outputs are not written); the
-                // env needs a reset, which the auto-reset modes do as for an
-                // ended episode (all_done set; SAME_STEP resets it right away)
-                if (l == 0 && p.err) p.err[e] |= GW_ERR_DOUBLE_REMOVE;
+                // the step raised (Grid.remove's KeyError, the attack's
+                // ValueError): it stops there (no further attacks or moves, no
+                // observation draws, its outputs are not written); the env needs
+                // a reset, which the auto-reset modes do as for an ended episode
+                // (all_done set; SAME_STEP resets it right away)
+                if (l == 0 && p.err) p.err[e] |= raised;
                 steps += 1;
                 acting_sum += (uint64_t)__popcll(act_mask);
                 if (p.autoreset && l == 0) ad_t[e] = 1;
@@ -2884,11 +2907,12 @@ __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
                 const uint32_t amap = (uint32_t)uni(arg[1]);
                 const uint32_t keep = L.amap;
                 if (l == a) L.amap = amap;                  // attack_mapping[attacker's encoding]
+                bool nd = false;
                 const bool st = (f & 2)
                     ? attack_selective(q, sm, rng, L, a, arg + 2, nlist, list)
-                    : attack_one(q, sm, rng, L, a, uni(arg[2]), nlist, list);
+                    : attack_one(q, sm, rng, L, a, uni(arg[2]), nlist, list, &nd);
                 if (l == a) L.amap = keep;
-                status = st ? 1 : 0;
+                status = st ? (nd ? 3 : 1) : 0;             // bit 1: a numpy array (actor.py:412-414)
             }
         } else if (op == GW_OP_CROSS_MOVE || op == GW_OP_DRIFT_MOVE) {
             // CrossMoveActor / DriftMoveActor.process_action (actor.py:161-234):
@@ -3341,7 +3365,7 @@ static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 5; }
+int32_t gw_abi_version(void) { return 6; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
@@ -3606,6 +3630,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.obs_only = -1;
     p.comp_amap = -1;
     p.observe_self = cfg->observe_self; p.stacked = cfg->stacked_attacks;
+    p.arr_as_list = cfg->attack_array_as_list;
     p.no_overlap_at_reset = cfg->no_overlap_at_reset; p.state_order = cfg->state_order;
     p.done_kind = cfg->done_kind;
     for (int i = 0; i <= GW_MAX_ENC; i++) { p.overlap[i] = cfg->overlap[i]; p.amap[i] = cfg->attack_mapping[i]; }

@@ -542,6 +542,11 @@ class GridWorldEngine:
             e = int(np.nonzero(err & _abi.GW_ERR_DOUBLE_REMOVE)[0][0])
             raise KeyError(f"Grid.remove of an agent no longer in the grid (env {e}; "
                            f"reach_the_target.py:118-120)")
+        if (err & _abi.GW_ERR_VALUE_ERROR).any():
+            e = int(np.nonzero(err & _abi.GW_ERR_VALUE_ERROR)[0][0])
+            raise ValueError(f"The truth value of an array with more than one element is ambiguous. "
+                             f"Use a.any() or a.all() (env {e}: `not attacked_agents` on "
+                             f"BinaryAttackActor's numpy array, team_battle_example.py:41)")
 
     # ------------------------------------------------------------ state
     def get_state(self):

@@ -204,4 +204,9 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
     # reference does, and hands the order to the engine
     # (gw_set_placement_order; the dict-level API, one env per runtime)
     cc.randomize_placement_order = bool(pos_states[0].randomize_placement_order)
+    # the reference's TeamBattle / ReachTheTarget steps raise ValueError when
+    # BinaryAttackActor returns a numpy array of 2 or more agents (`not
+    # attacked_agents`, team_battle_example.py:41); a simulation whose
+    # `attack_array_as_list` is True opts into the list reading instead
+    cc.cfg.attack_array_as_list = int(bool(getattr(sim, 'attack_array_as_list', False)))
     return cc

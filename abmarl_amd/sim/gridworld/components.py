@@ -375,6 +375,13 @@ class AttackActorBaseComponent(ActorBaseComponent, ABC):
         status, attacked, _ = ComponentRuntime.of(self).op(
             _abi.GW_OP_ATTACK, attacking_agent,
             [flags, amap] + list(self._attack_args(action_dict[self.key])))
+        if status & 2:
+            # _subset_attackables' np.random.choice returns a numpy array
+            # (actor.py:412-414), which the ammo filter did not turn into a
+            # list: returned as one, so `not attacked` behaves as there
+            arr = np.empty(len(attacked), dtype=object)
+            arr[:] = attacked
+            return True, arr
         return bool(status), attacked
 
     def _attack_args(self, action):

@@ -105,6 +105,13 @@ typedef int32_t gw_status;
 #define GW_ERR_NOT_IN_GRID   16u  /* gw_component MOVE of an entity that is not in the grid:
                                      Grid.remove raises KeyError (actor.py:108-110);
                                      the entity stays where it was                    */
+#define GW_ERR_VALUE_ERROR   32u  /* TeamBattle / ReachTheTarget step with BinaryAttackActor:
+                                     `not attacked_agents` on the numpy array of 2 or more
+                                     picks _subset_attackables returns (actor.py:412-414)
+                                     raises ValueError (team_battle_example.py:41,
+                                     reach_the_target.py:107); the step stops after that
+                                     attacker's attack (damage, ammo and draws applied)
+                                     unless gw_config.attack_array_as_list              */
 
 /* ------------------------------------------------------------ agent kinds */
 /* bit flags describing which reference mixins an entity derives from        */
@@ -232,6 +239,13 @@ typedef struct gw_config {
     /* 1: a component-API handle (gw_component only, no step program): either
        attack kind on the workgroup-per-env engine above 64 lanes           */
     int32_t  component_api;
+    /* 0 (the reference): an attacker whose BinaryAttackActor returns the numpy
+       array of 2 or more picks makes the step's `not attacked_agents` raise
+       ValueError (GW_ERR_VALUE_ERROR; TeamBattle and ReachTheTarget programs).
+       1 (opt-in): the attacked agents are read as a list, `len(...) == 0`
+       being the failed-attack test -- the example's evident meaning, which
+       the reference itself cannot run.                                      */
+    int32_t  attack_array_as_list;
 } gw_config;
 
 /* Width of one entity's action: {move_row, move_col, attack...}.  The attack

@@ -14,7 +14,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_walls',
                 'tb_destroy', 'tb_chase', 'tb_views', 'maze_file', 'maze_16', 'rtt_7', 'rtt_7_views',
                 'rtt_16', 'rtt_double', 'rtt_64', 'traffic_ex', 'traffic_9', 'tb_128', 'tb_100',
-                'rtt_16_example', 'tb_ammo', 'tb_ammo_multi', 'tb_ammo_stacked', 'rtt_ammo']
+                'rtt_16_example', 'tb_ammo', 'tb_ammo_multi', 'tb_ammo_stacked', 'rtt_ammo',
+                'tb_value_error', 'tb_value_error_ammo']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):
@@ -162,7 +163,12 @@ def build_sim(c, sim_cls=None):
         return (sim_cls or TeamBattleSim).build_sim_from_array(
             arr, {'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=wenc, blocking=True)},
             extra_agents=agents, **kwargs)
-    return (sim_cls or TeamBattleSim).build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
+    sim = (sim_cls or TeamBattleSim).build_sim(c['rows'], c['cols'], agents=agents, **kwargs)
+    if c.get('len_fix'):
+        # the fixture ran the example with `len(attacked_agents) == 0` for its
+        # failed-attack test (make_golden.py len_fixed_team_battle): the opt-in
+        sim.attack_array_as_list = True
+    return sim
 
 
 def team_battle(rows=32, cols=32, n_agents=64, n_teams=2, **kw):

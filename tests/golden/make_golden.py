@@ -191,6 +191,21 @@ CASES = [
          horizon=40, seed_base=203, ammo=[2, 4], attack_max=2, stacked_attacks=True, len_fix=True,
          agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=1,
                     view_range=2, simultaneous_attacks=2)),
+    # the reference's own TeamBattleSim with simultaneous_attacks 3: whenever
+    # _subset_attackables returns np.random.choice's array of two or more
+    # agents (actor.py:412-414), `not attacked_agents` (team_battle_example.py:41)
+    # raises ValueError -- recorded per env-step like the KeyError (err = 2),
+    # after the attack's damage and draws; the env is then reset
+    dict(name='tb_value_error', rows=7, cols=7, n_agents=14, n_teams=2, n_envs=6, n_steps=140,
+         horizon=45, seed_base=211, attack_max=3, overlap={1: [1, 2], 2: [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=2, simultaneous_attacks=3)),
+    # stacked attacks (choice with replacement: an array for any candidate
+    # count) and AmmoAgents, whose filter turns a longer list into a list
+    dict(name='tb_value_error_ammo', rows=6, cols=6, n_agents=10, n_teams=2, n_envs=6, n_steps=120,
+         horizon=40, seed_base=213, ammo=[1, 3], attack_max=2, stacked_attacks=True,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=1,
+                    view_range=2, simultaneous_attacks=2)),
     # ReachTheTarget whose target is an AmmoAgent (SelectiveAttackActor: two
     # attacks per cell of its window) and an AmmoState beside the example's states
     dict(name='rtt_ammo', kind='rtt', rows=9, cols=9, n_barriers=8, n_runners=20, n_envs=4,
@@ -560,10 +575,12 @@ def run_case(case):
                                       'attack': int(act[t, e, i, 2])}
             try:
                 o, r, d, _ = m.step(adict)
-            except KeyError:
-                # reach_the_target.py:118-120, Grid.remove of a runner the
-                # target already killed on its cell: the env must be reset
-                out['err'][t, e] = 1
+            except (KeyError, ValueError) as ex:
+                # KeyError (err 1): reach_the_target.py:118-120, Grid.remove of a
+                # runner the target already killed on its cell; ValueError (err
+                # 2): `not attacked_agents` on BinaryAttackActor's numpy array
+                # (team_battle_example.py:41).  The env must be reset.
+                out['err'][t, e] = 1 if isinstance(ex, KeyError) else 2
                 steps[e] = c['horizon']
                 out['mt_pos'][t, e] = np.random.get_state()[2]
                 out['mt_crc'][t, e] = zlib.crc32(np.ascontiguousarray(np.random.get_state()[1],

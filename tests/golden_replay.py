@@ -13,11 +13,14 @@ def check_step(g, t, obs, rew, done, all_done, state=None, where='', errors=None
     ReachTheTarget's double remove) have no reference outputs: for them only
     the error flag and the RNG state are checked."""
     E = g['all_done'].shape[1]
-    err = g['err'][t].astype(bool) if 'err' in g else np.zeros(E, bool)
+    code = g['err'][t] if 'err' in g else np.zeros(E, np.uint8)
+    err = code != 0
     if err.any():
+        # the fixture's exception (1 KeyError, 2 ValueError) -> the engine's flag
         assert errors is not None, f"{where} step {t}: runner reports no errors"
-        assert ((errors[err] & 4) != 0).all(), f"{where} step {t}: KeyError flag missing"
-        assert ((errors[~err] & 4) == 0).all(), f"{where} step {t}: spurious KeyError flag"
+        for c, flag, name in ((1, 4, 'KeyError'), (2, 32, 'ValueError')):
+            assert ((errors[code == c] & flag) != 0).all(), f"{where} step {t}: {name} flag missing"
+            assert ((errors[code != c] & flag) == 0).all(), f"{where} step {t}: spurious {name} flag"
         g = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in g.items()}
         g['obs'][t][err] = obs[err]
         g['reward'][t][err] = rew[err]

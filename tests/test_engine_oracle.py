@@ -11,13 +11,17 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(oracle_mod, cc, E, T, horizon, seed_run, key, check_every=1, force_workgroup=False,
-         env_per_lane=0, kernel=None):
+         env_per_lane=0, kernel=None, as_list=False):
     """The oracle holds every entity, the engine one lane per dynamic entity:
-    compare the lanes (static entities are constant in both)."""
+    compare the lanes (static entities are constant in both).  as_list: the
+    attacked agents read as a list (gw_config.attack_array_as_list) -- configs
+    attacking 2-3 times a step, whose reference step would raise ValueError
+    (that path: test_team_battle_value_error)."""
     import torch
     from abmarl_amd.engine import GridWorldEngine, env_seeds
     seeds = env_seeds(E, run=seed_run)
     cc.cfg.force_workgroup = int(force_workgroup)
+    cc.cfg.attack_array_as_list = int(as_list)
     cc.cfg.env_per_lane = int(env_per_lane)
     eng = GridWorldEngine(cc, E, seeds=seeds)
     assert eng.wg == (bool(force_workgroup) or eng.A > 64)
@@ -87,7 +91,7 @@ def test_dense_attack_configs(oracle_mod, kw):
 ])
 def test_dense_configs(oracle_mod, kw):
     cc = team_battle(**kw)
-    _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3)
+    _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, as_list=True)
 
 
 @pytest.mark.parametrize('kw', [
@@ -102,7 +106,7 @@ def test_team_battle_beyond_one_wave(oracle_mod, kw):
     """TeamBattle with more than 64 fighters: the workgroup-per-env kernel vs
     the oracle at 1024 envs."""
     cc = team_battle(**kw)
-    _run(oracle_mod, cc, E=1024, T=120, horizon=60, seed_run=12, key=29, check_every=2)
+    _run(oracle_mod, cc, E=1024, T=120, horizon=60, seed_run=12, key=29, check_every=2, as_list=True)
 
 
 @pytest.mark.parametrize('idx', [0, 3])
@@ -114,7 +118,7 @@ def test_dense_configs_workgroup_kernel(oracle_mod, idx):
                agent=dict(move_range=1, attack_range=1, attack_strength=0.4, attack_accuracy=0.9,
                           view_range=2, simultaneous_attacks=3))][idx]
     cc = team_battle(**kw)
-    _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, force_workgroup=True)
+    _run(oracle_mod, cc, E=512, T=150, horizon=40, seed_run=5, key=3, force_workgroup=True, as_list=True)
 
 
 @pytest.mark.parametrize('waves', [2, 4])
@@ -198,7 +202,7 @@ def test_mixed_view_configs(oracle_mod, kw):
 ])
 def test_blocking_configs(oracle_mod, kw):
     cc = team_battle(**kw)
-    _run(oracle_mod, cc, E=512, T=150, horizon=50, seed_run=7, key=9)
+    _run(oracle_mod, cc, E=512, T=150, horizon=50, seed_run=7, key=9, as_list=True)
 
 
 def test_generic_window_resets_cross_the_twist(oracle_mod):
@@ -281,10 +285,17 @@ RTT_WAVE_CASES = [
 def _run_rtt(oracle_mod, kw, E, T, horizon, run=11, key=23, min_errs=0, force_workgroup=False):
     """ReachTheTarget (SelectiveAttackActor, TargetDone, OnlyAgentLeftDone)
     engine vs oracle; an env whose step raised (double remove) is reset by both."""
-    import torch
-    from abmarl_amd.engine import GridWorldEngine, env_seeds
     from tests.cases import build_rtt
     cc = build_rtt(dict(kind='rtt', **kw)).compiled()
+    return _run_raising(oracle_mod, cc, E, T, horizon, run, key, min_errs, force_workgroup, flag=4)
+
+
+def _run_raising(oracle_mod, cc, E, T, horizon, run, key, min_errs=0, force_workgroup=False, flag=4):
+    """Engine vs oracle for a program whose step can raise (err `flag`: 4 the
+    double remove's KeyError, 32 the attack's ValueError): the raising envs'
+    flags and RNG must agree, then both reset them."""
+    import torch
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
     cc.cfg.force_workgroup = int(force_workgroup)
     seeds = env_seeds(E, run=run)
     eng = GridWorldEngine(cc, E, seeds=seeds)
@@ -303,9 +314,10 @@ def _run_rtt(oracle_mod, kw, E, T, horizon, run=11, key=23, min_errs=0, force_wo
         eng.err.zero_()
         orc.step(h_act, o_obs, rew, done, ad)
         obs, r, d, a = eng.step(act)
-        e_err = (eng.err.cpu().numpy() & 4) != 0
-        o_err = (orc.errors() & 4) != 0
-        assert (e_err == o_err).all(), f"step {t}: KeyError flags"
+        e_err = (eng.err.cpu().numpy() & flag) != 0
+        o_err = (orc.errors() & flag) != 0
+        assert (e_err == o_err).all(), f"step {t}: error flags"
+        assert not ((eng.err.cpu().numpy() | orc.errors()) & ~flag).any(), f"step {t}: other flags"
         ok = ~o_err
         errs += int(o_err.sum())
         assert (a.cpu().numpy()[ok] == ad[ok]).all(), f"step {t}: __all__"
@@ -439,3 +451,35 @@ def test_reach_the_target_config4_autoreset(oracle_mod):
         mt = eng.get_state()['mt'].cpu().numpy().view(np.uint32)
         assert (mt[:, :625] == orc.state()['mt'][:, :625]).all(), f"{mode}: RNG"
         assert errs > 0, "config 4 places runners on the target's cell: some steps raise"
+
+
+@pytest.mark.parametrize('force_workgroup', [False, True])
+@pytest.mark.parametrize('kw', [
+    # simultaneous_attacks 3, accuracy < 1: np.random.choice's array of 2 or 3
+    # picks whenever there are at least as many candidates as attacks
+    dict(rows=8, cols=8, n_agents=40, n_teams=2, overlap={'1': [1, 2], '2': [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.8,
+                    view_range=2, simultaneous_attacks=3)),
+    # stacked: an array for any candidate count
+    dict(rows=10, cols=10, n_agents=30, n_teams=3, stacked_attacks=True,
+         agent=dict(move_range=1, attack_range=2, attack_strength=0.4, attack_accuracy=1,
+                    view_range=3, simultaneous_attacks=2)),
+])
+def test_team_battle_value_error(oracle_mod, kw, force_workgroup):
+    """The reference's TeamBattleSim.step raises ValueError on `not
+    attacked_agents` when BinaryAttackActor returns np.random.choice's array
+    of 2 or more agents (team_battle_example.py:41, actor.py:412-414): both
+    kernels flag GW_ERR_VALUE_ERROR at that attacker, with the attack's damage
+    and draws applied and the step stopped, as the oracle does."""
+    cc = team_battle(**kw)
+    _run_raising(oracle_mod, cc, E=1024, T=60, horizon=30, run=21, key=41, min_errs=50,
+                 force_workgroup=force_workgroup, flag=32)
+
+
+def test_team_battle_value_error_opt_out(oracle_mod):
+    """gw_config.attack_array_as_list = 1 (a simulation with
+    attack_array_as_list = True): the list reading, no raise."""
+    cc = team_battle(rows=8, cols=8, n_agents=40, n_teams=2, overlap={'1': [1, 2], '2': [2, 1]},
+                     agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.8,
+                                view_range=2, simultaneous_attacks=3))
+    _run(oracle_mod, cc, E=1024, T=60, horizon=30, seed_run=21, key=41, as_list=True)

@@ -17,3 +17,6 @@ rc=$?; grep -v amdgpu.ids gpurun_out/r05a/split_probe.log; [ $rc -eq 0 ] || exit
 GW_ENGINE_VARIANT=checks timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
   --timeout 120 --timeout-method thread -k "$SEL" > gpurun_out/r05a/head_checks.log 2>&1
 rc=$?; tail -2 gpurun_out/r05a/head_checks.log; [ $rc -eq 0 ] || { echo "HEAD CHECKS rc=$rc"; tail -40 gpurun_out/r05a/head_checks.log; exit 1; }
+# 3. HEAD's production build: the whole GPU suite
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05a/head_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/r05a/head_gpu.log; [ $rc -eq 0 ] || { echo "HEAD GPU rc=$rc"; tail -40 gpurun_out/r05a/head_gpu.log; exit 1; }
