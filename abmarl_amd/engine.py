@@ -81,7 +81,7 @@ class GridWorldEngine:
             self.L.gw_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
             self.L.gw_debug_set_stamps(self.h, _ptr(self.stamps))
         if _native.VARIANT == 'checks':
-            self._dbg = torch.zeros(16, dtype=torch.int32, device=dev)
+            self._dbg = torch.zeros(256, dtype=torch.int32, device=dev)   # [0..15] checks; the rest diagnostic builds
             self.L.gw_debug_set_checks.argtypes = [C.c_void_p, C.c_void_p]
             self.L.gw_debug_set_checks(self.h, _ptr(self._dbg))
         self.seed(env_seeds(E) if seeds is None else seeds)

@@ -32,7 +32,10 @@ the reference's len(action_dict), over all ranks / the max
 wall time over ranks.  The engine counts acting agents on device.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
-       N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+       N > 1 launches N ranks itself (torch.distributed.run, one process per
+       GPU, RCCL) unless it already runs under a launcher that set WORLD_SIZE,
+       which must then equal N:
+       python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
 import argparse
 import json
@@ -339,6 +342,39 @@ WORKLOADS = {
 }
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` outside a launcher: start the N ranks as
+    `torch.distributed.run --nproc-per-node N` children (rendezvous on
+    127.0.0.1) and return their exit code.  Called before anything touches
+    the GPU (torch.cuda.device_count() does not initialise it)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, cwd=ROOT)
+
+
+def check_world(gpus):
+    """The rank layout --gpus N asks for: None when this process is one of the
+    N ranks (or N == 1), 'launch' when it must start them, else an error."""
+    world = os.environ.get('WORLD_SIZE')
+    if gpus < 1:
+        return f'--gpus {gpus}: at least one GPU'
+    if world is not None:
+        if int(world) != gpus:
+            return f'--gpus {gpus} but WORLD_SIZE={world}: the launcher and --gpus disagree'
+        return None
+    if gpus == 1:
+        return None
+    ndev = torch.cuda.device_count()
+    if gpus > ndev:
+        return f'--gpus {gpus} but this node has {ndev} visible GPU(s)'
+    return 'launch'
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -379,6 +415,13 @@ def main():
                          'one-wave kernel')
     args = ap.parse_args()
 
+    # --gpus N: N ranks, launched here if no launcher did (before any GPU call)
+    chk = check_world(args.gpus)
+    if chk == 'launch':
+        sys.exit(launch_ranks(args.gpus))
+    if chk is not None:
+        print(f'bench.py: {chk}', file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))

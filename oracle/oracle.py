@@ -49,6 +49,7 @@ def lib():
         L.gwo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.gwo_step_masked.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
         L.gwo_get_err.argtypes = [vp, vp]
+        L.gwo_set_steps.argtypes = [vp, vp]
         L.gwo_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
         L.gwo_get_cells.argtypes = [vp, C.c_int32, vp]
         L.gwo_get_ammo.argtypes = [vp, vp]
@@ -156,6 +157,11 @@ class Oracle:
         out = np.zeros(self.E, np.float64)
         self.L.gwo_take_reward(self.h, int(entity), _p(out))
         return out
+
+    def set_steps(self, steps):
+        """Steps since reset per env (the engine's set_state(steps=...))."""
+        steps = np.ascontiguousarray(steps, dtype=np.int32)
+        self.L.gwo_set_steps(self.h, _p(steps))
 
     def errors(self):
         out = np.zeros(self.E, np.uint32)

@@ -1,14 +1,13 @@
 """A trajectory of user components registered beside the REFERENCE's
-built-in components (tests/user_comms.py: a message-broadcasting simulation
-in the manner of the reference's examples/sim/comms_blocking.py), run in this
-container on the reference's PositionState / MoveActor /
-PositionCenteredEncodingObserver / create_grid_and_mask under its
-AllStepManager.
+built-in components (tests/user_lanterns.py: lantern keepers sharing oil
+with the keepers they can see, blocking wanderers), run in this container on
+the reference's PositionState / MoveActor / PositionCenteredEncodingObserver /
+create_grid_and_mask under its AllStepManager.
 
-Output: tests/golden/comms_blocking.json -- per env the seed, and after
-reset and every step the actions, observations (grid windows and message
-dicts), rewards, dones, positions, messages and the numpy RNG position + key
-CRC.  Floats are stored as float.hex (bit-exact).
+Output: tests/golden/lanterns.json -- per env the seed, and after reset and
+every step the actions, observations (grid windows and oil readings),
+rewards, dones, positions, oil levels and the numpy RNG position + key CRC.
+Floats are stored as float.hex (bit-exact).
 Run:  python tests/golden/make_comms.py      (needs /root/reference)
 """
 import json
@@ -33,8 +32,8 @@ def enc_obs(o):
         e = {}
         if 'position_centered_encoding' in d:
             e['grid'] = np.asarray(d['position_centered_encoding']).astype(int).tolist()
-        if 'message' in d:
-            e['message'] = {k: fhex(v) for k, v in d['message'].items()}
+        if 'oil' in d:
+            e['oil'] = [fhex(v) for v in d['oil']]
         out[aid] = e
     return out
 
@@ -42,7 +41,7 @@ def enc_obs(o):
 def snapshot(sim):
     st = np.random.get_state()
     return dict(pos={a.id: [int(x) for x in a.position] for a in sim.agents.values()},
-                message={a.id: fhex(a.message) for a in sim.agents.values() if hasattr(a, '_message')},
+                oil={a.id: fhex(a.oil) for a in sim.agents.values() if hasattr(a, '_oil')},
                 mt_pos=int(st[2]),
                 mt_crc=zlib.crc32(np.ascontiguousarray(st[1], dtype=np.uint32).tobytes()))
 
@@ -67,23 +66,23 @@ def main():
     import gym_stub
     gym_stub.install()
     sys.path.insert(0, REF)
-    import user_comms
+    import user_lanterns
     from abmarl.managers import AllStepManager
     from abmarl.sim.gridworld.registry import register, registry
-    classes = user_comms.comms_classes(reference_namespace())
-    for k in ('BroadcastingState', 'BroadcastingActor', 'BroadcastObserver', 'AverageMessageDone'):
+    classes = user_lanterns.lantern_classes(reference_namespace())
+    for k in user_lanterns.USER_COMPONENTS:
         register(classes[k])
-    assert classes['BroadcastObserver'] in registry['observer'].values()
-    c = user_comms.CASE
+    assert classes['OilGauge'] in registry['observer'].values()
+    c = user_lanterns.CASE
     rng = np.random.RandomState(c['action_seed'])
     envs = []
     for seed in c['seeds']:
-        sim = user_comms.build(classes)
+        sim = user_lanterns.build(classes)
         m = AllStepManager(sim)
         np.random.seed(seed)
         rec = dict(seed=seed, reset=dict(obs=enc_obs(m.reset()), **snapshot(sim)), steps=[])
         for t in range(c['n_steps']):
-            acts = user_comms.actions(sim, rng, m.done_agents)
+            acts = user_lanterns.actions(sim, rng, m.done_agents)
             o, r, d, _ = m.step(acts)
             rec['steps'].append(dict(
                 actions={k: {kk: (np.asarray(vv).tolist()) for kk, vv in v.items()} for k, v in acts.items()},
@@ -92,9 +91,9 @@ def main():
             if d['__all__']:
                 break
         envs.append(rec)
-    path = os.path.join(HERE, 'comms_blocking.json')
+    path = os.path.join(HERE, 'lanterns.json')
     json.dump(dict(case=c, envs=envs), open(path, 'w'))
-    print(f"comms_blocking: {len(envs)} envs, {[len(e['steps']) for e in envs]} steps -> "
+    print(f"lanterns: {len(envs)} envs, {[len(e['steps']) for e in envs]} steps -> "
           f"{os.path.getsize(path)} B")
 
 

@@ -8,10 +8,11 @@ Evidence:
     refused with TypeError);
   * create_grid_and_mask (the host form user components call) against 400
     masks the reference computed (tests/golden/make_masks.py);
-  * on the GPU, a message-broadcasting simulation built from user
-    components (tests/user_comms.py) replays the trajectory the reference's
-    built-ins produced with the same user code (tests/golden/make_comms.py):
-    grid windows, messages, rewards, dones, positions and the numpy stream.
+  * on the GPU, a simulation built from user components (tests/user_lanterns.py:
+    lantern keepers sharing oil in sight of each other, blocking wanderers)
+    replays the trajectory the reference's built-ins produced with the same
+    user code (tests/golden/make_comms.py): grid windows, oil readings,
+    rewards, dones, positions and the numpy stream.
 """
 import json
 import os
@@ -23,7 +24,7 @@ import pytest
 
 from abmarl_amd.sim.gridworld.registry import registry, register
 from abmarl_amd.sim.gridworld import components as comp
-from tests import user_comms
+from tests import user_lanterns
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
@@ -57,18 +58,16 @@ def test_built_in_registry():
 def test_custom_registrations():
     """test_registry.py:43-55: user components register by type and name; an
     agent class is not a component."""
-    classes = user_comms.comms_classes(our_namespace())
-    register(classes['BroadcastingState'])
-    register(classes['BroadcastingActor'])
-    register(classes['BroadcastObserver'])
-    register(classes['AverageMessageDone'])
-    assert classes['BroadcastingState'] in registry['state'].values()
-    assert classes['BroadcastingActor'] in registry['actor'].values()
-    assert classes['BroadcastObserver'] in registry['observer'].values()
-    assert classes['AverageMessageDone'] in registry['done'].values()
-    assert registry['actor']['BroadcastingActor'] is classes['BroadcastingActor']
+    classes = user_lanterns.lantern_classes(our_namespace())
+    for k in user_lanterns.USER_COMPONENTS:
+        register(classes[k])
+    assert classes['OilStock'] in registry['state'].values()
+    assert classes['PourActor'] in registry['actor'].values()
+    assert classes['OilGauge'] in registry['observer'].values()
+    assert classes['EvenOilDone'] in registry['done'].values()
+    assert registry['actor']['PourActor'] is classes['PourActor']
     with pytest.raises(TypeError):
-        register(classes['BroadcastingAgent'])
+        register(classes['Keeper'])
 
 
 def test_program_sims_refuse_user_components():
@@ -77,12 +76,12 @@ def test_program_sims_refuse_user_components():
     from abmarl_amd.examples import TeamBattleSim
     from abmarl_amd.sim.gridworld.compile import UnsupportedConfig
     from tests.cases import Fighter
-    classes = user_comms.comms_classes(our_namespace())
-    register(classes['BroadcastingState'])
+    classes = user_lanterns.lantern_classes(our_namespace())
+    register(classes['OilStock'])
     agents = {f'a{i}': Fighter(id=f'a{i}', encoding=1 + i % 2, move_range=1, attack_range=1,
                                attack_strength=1, attack_accuracy=1, view_range=2) for i in range(4)}
     sim = TeamBattleSim.build_sim(5, 5, agents=agents, attack_mapping={1: {2}, 2: {1}},
-                                  states={'PositionState', 'HealthState', 'BroadcastingState'},
+                                  states={'PositionState', 'HealthState', 'OilStock'},
                                   observers={'PositionCenteredEncodingObserver'},
                                   dones={'OneTeamRemainingDone'})
     with pytest.raises(UnsupportedConfig):
@@ -125,9 +124,9 @@ def test_user_components_replay_reference():
     trajectory of the same user code bit-exactly."""
     from abmarl_amd.managers import AllStepManager
     from abmarl_amd.sim.gridworld.component_runtime import ComponentRuntime
-    d = json.load(open(os.path.join(GOLDEN, 'comms_blocking.json')))
-    classes = user_comms.comms_classes(our_namespace())
-    for k in ('BroadcastingState', 'BroadcastingActor', 'BroadcastObserver', 'AverageMessageDone'):
+    d = json.load(open(os.path.join(GOLDEN, 'lanterns.json')))
+    classes = user_lanterns.lantern_classes(our_namespace())
+    for k in user_lanterns.USER_COMPONENTS:
         register(classes[k])
     h = float.fromhex
 
@@ -137,20 +136,19 @@ def test_user_components_replay_reference():
             if 'grid' in want:
                 np.testing.assert_array_equal(got['position_centered_encoding'], np.array(want['grid']),
                                               err_msg=where)
-            if 'message' in want:
-                assert {k: float(v) for k, v in got['message'].items()} == \
-                    {k: h(v) for k, v in want['message'].items()}, where
+            if 'oil' in want:
+                assert [float(v) for v in got['oil']] == [h(v) for v in want['oil']], where
         assert set(obs) == set(rec['obs']), where
         for aid, p in rec['pos'].items():
             assert list(map(int, sim.agents[aid].position)) == p, where
-        for aid, v in rec['message'].items():
-            assert sim.agents[aid].message == h(v), where
+        for aid, v in rec['oil'].items():
+            assert sim.agents[aid].oil == h(v), where
         st = np.random.get_state()
         assert st[2] == rec['mt_pos'], where
         assert zlib.crc32(np.ascontiguousarray(st[1], dtype=np.uint32).tobytes()) == rec['mt_crc'], where
 
     for env in d['envs']:
-        sim = user_comms.build(classes)
+        sim = user_lanterns.build(classes)
         m = AllStepManager(sim)
         np.random.seed(env['seed'])
         check(sim, m.reset(), env['reset'], f"seed {env['seed']} reset")
