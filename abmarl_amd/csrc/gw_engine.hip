@@ -174,6 +174,7 @@ struct Params {
     uint64_t agent_lanes;                  // lanes that are Agents (the turn cycle)
     // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
+    int32_t obs_lo, obs_hi;                // lanes [obs_lo, obs_hi) hold every grid observer
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
     int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
     int32_t persistent_obs;                // gw_config.persistent_obs: skip rows already -2
@@ -3578,7 +3579,9 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         hs[l].init_health = s.initial_health;
         hs[l].init_orient = s.initial_orientation;
         hs[l].tgt_lane = -1; hs[l].tgt_pos = 0; hs[l].dtgt_lane = -1;
-        hs[l].init_ammo = (s.kind & GW_K_AMMO) ? s.initial_ammo : 0;
+        // AmmoState.reset assigns initial_ammo through the ammo setter, which
+        // clamps to 0 (agent.py:308-311, state.py:651-656)
+        hs[l].init_ammo = (s.kind & GW_K_AMMO) ? (s.initial_ammo < 0 ? 0 : s.initial_ammo) : 0;
     }
     for (int l = 0; l < GW_MAX_LANES; l++) {
         g->policy.w[l] = l < A ? ((hs[l].kind & 0xffu) | ((uint32_t)(hs[l].move_range & 0xff) << 8) |
@@ -3817,6 +3820,12 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         p.nwv = (A + WAVE - 1) / WAVE;
         if (cfg->force_workgroup > p.nwv) p.nwv = cfg->force_workgroup;
         g->smem_step = g->smem_reset = wg_smem_bytes(HW, A, g->S, max_enc, p.tbl_rows * p.pitch, p.nwv);
+        // the lanes that can ever observe (skip_done_obs stores only their rows:
+        // config 4's 128 barriers are the first half of its lanes)
+        p.obs_lo = A; p.obs_hi = 0;
+        for (int l = 0; l < A; l++)
+            if (hs[l].kind & GW_K_GRID_OBSERVER) { if (l < p.obs_lo) p.obs_lo = l; p.obs_hi = l + 1; }
+        if (p.obs_hi == 0) p.obs_lo = 0;
         // moves run in parallel when every moving lane's encoding may share a
         // cell with every lane encoding (static cells are refused separately)
         uint32_t lane_encs = 0;
@@ -3915,8 +3924,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     // health, no blocking lane, the target a plain entity: one lane per env
     // (gw_lane.inc)
     {
+        // (no AmmoAgent: the lane kernel keeps no ammo, whose reset the one-wave
+        // kernel does as AmmoState.reset)
         bool able = maze && A == 2 && !pac && !wg && !big && !p.lane_blockers && !p.hetero_view && p.nav >= 0 &&
-                    p.target >= 0 && p.nav != p.target;
+                    p.target >= 0 && p.nav != p.target && !any_ammo;
         for (int l = 0; able && l < A; l++) {
             if (hs[l].init_r < 0 || hs[l].init_c < 0 || (hs[l].kind & GW_K_HEALTH)) able = false;
             if (l == p.target && (hs[l].kind & dynamic_kinds)) able = false;

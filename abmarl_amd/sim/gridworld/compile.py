@@ -71,6 +71,20 @@ def agent_spec(agent, program_type=None, food_type=None):
     return s
 
 
+# the component methods a fused program runs as device code
+_DEVICE_METHODS = ('reset', 'process_action', 'get_obs', 'get_done', 'get_all_done')
+
+
+def _overridden(obj, builtins):
+    """The device methods a subclass of a built-in component overrides: the
+    program would run the built-in's device form and silently ignore them."""
+    base = next((b for b in type(obj).__mro__ if b in builtins), None)
+    if base is None or type(obj) is base:
+        return []
+    return [m for m in _DEVICE_METHODS
+            if hasattr(base, m) and getattr(type(obj), m, None) is not getattr(base, m, None)]
+
+
 def compile_sim(sim, program, states, observers, dones, actors, state_order,
                 nav_agent=-1, target_agent=-1, program_type=None, food_type=None,
                 pacman_agent=-1, tunnel=(-1, -1, -1, -1), pac_rewards=(0, 0, 0, 0, 0)):
@@ -90,6 +104,18 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
     if sim.grid.rows * sim.grid.cols > _abi.GW_MAX_CELLS:
         raise UnsupportedConfig(f"grid larger than {_abi.GW_MAX_CELLS} cells")
 
+    builtins = (PositionState, HealthState, OrientationState, AmmoState, MoveActor, DriftMoveActor,
+                BinaryAttackActor, SelectiveAttackActor, PositionCenteredEncodingObserver,
+                AbsoluteEncodingObserver, ActiveDone, OneTeamRemainingDone, TargetAgentDone,
+                TargetDestroyedDone)
+    for x in list(states) + list(actors) + list(observers) + list(dones):
+        if getattr(x, '_program_done', None) == program:
+            continue                          # the sim program's own done component
+        over = _overridden(x, builtins)
+        if over:
+            raise UnsupportedConfig(f"{type(x).__name__} overrides {', '.join(over)} of a built-in "
+                                    "component: a fused program runs the built-in's device code "
+                                    "(run it through the component API instead)")
     for s in states:
         if isinstance(s, _TargetPlacementState):
             raise UnsupportedConfig(f"{type(s).__name__} runs through the component API "
@@ -107,6 +133,10 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
         # without AmmoState.reset the agent has no ammo: the reference raises
         # AttributeError at its first attack (actor.py:346)
         raise UnsupportedConfig("attacking AmmoAgents require an AmmoState")
+    if program == _abi.GW_SIM_PACMAN and any(isinstance(a, AmmoAgent) for a in agents):
+        # pac_kernel keeps no ammo lane state (nothing in the Pacman program
+        # attacks, so AmmoState.reset would be its only use)
+        raise UnsupportedConfig("AmmoAgents have no HIP implementation in the Pacman program")
 
     obs_range = 0
     observe_self = True

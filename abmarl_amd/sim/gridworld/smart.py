@@ -85,9 +85,13 @@ class SmartGridWorldSimulation(GridWorldSimulation, ABC):
         assert self._engine_program is not None, \
             f"{type(self).__name__} has no engine step program"
         # the states of the sets, and those a subclass holds as attributes
-        # (e.g. an AmmoState added to an example program)
+        # (e.g. an AmmoState added to an example program) whose type the sets
+        # do not already hold (an attribute twin of a set's PositionState is
+        # the same component kind, reset once by the program)
+        held = {type(s) for s in self._states}
         states = list(self._states) + [v for v in vars(self).values()
-                                       if isinstance(v, StateBaseComponent) and v not in self._states]
+                                       if isinstance(v, StateBaseComponent) and v not in self._states
+                                       and type(v) not in held]
         return compile_sim(self, self._engine_program, states, self._observers,
                            self._dones, self._actors(), self.state_order,
                            **self._program_extras())

@@ -15,7 +15,7 @@ GOLDEN_CASES = ['tb_small', 'tb_mixed', 'tb_order', 'tb_32', 'tb_corners', 'tb_w
                 'tb_destroy', 'tb_chase', 'tb_views', 'maze_file', 'maze_16', 'rtt_7', 'rtt_7_views',
                 'rtt_16', 'rtt_double', 'rtt_64', 'traffic_ex', 'traffic_9', 'tb_128', 'tb_100',
                 'rtt_16_example', 'tb_ammo', 'tb_ammo_multi', 'tb_ammo_stacked', 'rtt_ammo',
-                'tb_value_error', 'tb_value_error_ammo']
+                'tb_value_error', 'tb_value_error_ammo', 'tb_ammo_negative']
 
 
 class Fighter(GridObservingAgent, MovingAgent, AttackingAgent, HealthAgent):

@@ -175,6 +175,13 @@ CASES = [
          seed_base=201, ammo=[1, 3, 2], overlap={1: [1, 2], 2: [2, 1]},
          agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.9,
                     view_range=2)),
+    # a negative initial_ammo: AmmoState.reset assigns it through the ammo
+    # setter, which clamps to 0 (agent.py:308-311), so those fighters' attacks
+    # keep choice(attacked, 0) = nothing and cost -0.1
+    dict(name='tb_ammo_negative', rows=7, cols=7, n_agents=14, n_teams=2, n_envs=4, n_steps=120,
+         horizon=40, seed_base=217, ammo=[-2, 1, 0, 3], overlap={1: [1, 2], 2: [2, 1]},
+         agent=dict(move_range=1, attack_range=1, attack_strength=0.5, attack_accuracy=0.9,
+                    view_range=2)),
     # several attacks a step (simultaneous_attacks 3, stacked or not), so the
     # ammo filter draws its permutation over longer attacked lists.  The
     # reference's TeamBattleSim.step tests `not attacked_agents`

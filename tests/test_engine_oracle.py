@@ -144,6 +144,37 @@ def test_maze_navigation_1024_envs(oracle_mod, kernel):
          kernel=_abi.GW_KERNEL_LANE if kernel == 'lane' else _abi.GW_KERNEL_WAVE)
 
 
+def test_maze_navigation_ammo_navigator(oracle_mod):
+    """An AmmoAgent navigator (with an AmmoState): the lane-per-env kernel
+    keeps no ammo, so the config runs on the one-wave kernel, whose reset is
+    AmmoState.reset -- every env's navigator holds its initial_ammo."""
+    import torch
+    from abmarl_amd import _abi
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    from abmarl_amd.examples import MazeNavigationSim, MazeNavigationAgent
+    from abmarl_amd.sim.gridworld.agent import GridWorldAgent, AmmoAgent
+
+    class AmmoNavigator(MazeNavigationAgent, AmmoAgent):
+        pass
+
+    c = load_golden('maze_16')['case']
+    reg = {'N': lambda n: AmmoNavigator(id='navigator', encoding=1, view_range=c['agent']['view_range'],
+                                        initial_ammo=7),
+           'T': lambda n: GridWorldAgent(id='target', encoding=3),
+           'W': lambda n: GridWorldAgent(id=f'wall{n}', encoding=2, blocking=True)}
+    sim = MazeNavigationSim.build_sim_from_array(
+        np.array(c['maze'], dtype=object), reg, overlapping={1: {3}, 3: {1}},
+        states={'PositionState', 'AmmoState'}, observers={'PositionCenteredEncodingObserver'})
+    cc = sim.compiled()
+    eng = GridWorldEngine(cc, 64, seeds=env_seeds(64))
+    assert eng.kernel == _abi.GW_KERNEL_WAVE
+    eng.reset()
+    lane = list(eng.lane_entities).index(list(sim.agents).index('navigator'))
+    assert (eng.get_ammo().cpu().numpy()[:, lane] == 7).all()
+    torch.cuda.synchronize()
+    _run(oracle_mod, cc, E=512, T=150, horizon=60, seed_run=4, key=6, kernel=_abi.GW_KERNEL_WAVE)
+
+
 @pytest.mark.parametrize('kw', [
     # TargetDestroyedDone (+ ActiveDone): hunt the next fighter of the other team
     dict(rows=12, cols=12, n_agents=30, n_teams=2, dones=['ActiveDone', 'TargetDestroyedDone'],

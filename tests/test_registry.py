@@ -162,3 +162,52 @@ def test_user_components_replay_reference():
             check(sim, o, rec, where)
             assert {k: float(v) for k, v in r.items()} == {k: h(v) for k, v in rec['reward'].items()}, where
             assert {k: bool(v) for k, v in dn.items()} == rec['done'], where
+
+
+def test_overriding_subclass_of_a_built_in_is_refused():
+    """A fused program runs the built-in components' device code: a user
+    subclass that overrides one of their methods (here PositionState.reset)
+    would be ignored silently, so compiling refuses it; a subclass that only
+    renames keeps compiling."""
+    from abmarl_amd.examples import TeamBattleSim
+    from abmarl_amd.sim.gridworld.compile import UnsupportedConfig
+    from abmarl_amd.sim.gridworld.components import PositionState
+    from tests.cases import Fighter
+
+    class MyPosition(PositionState):
+        def reset(self, **kwargs):
+            super().reset(**kwargs)
+
+    class SamePosition(PositionState):
+        pass
+
+    register(MyPosition)
+    register(SamePosition)
+    agents = {f'a{i}': Fighter(id=f'a{i}', encoding=1 + i % 2, move_range=1, attack_range=1,
+                               attack_strength=1, attack_accuracy=1, view_range=2) for i in range(4)}
+    kw = dict(agents=agents, attack_mapping={1: {2}, 2: {1}}, observers={'PositionCenteredEncodingObserver'},
+              dones={'OneTeamRemainingDone'})
+    sim = TeamBattleSim.build_sim(5, 5, states={'MyPosition', 'HealthState'}, **kw)
+    with pytest.raises(UnsupportedConfig, match='overrides reset'):
+        sim.compiled()
+    TeamBattleSim.build_sim(5, 5, states={'SamePosition', 'HealthState'}, **kw).compiled()
+
+
+def test_attribute_state_twin_is_not_compiled_twice():
+    """A simulation that also keeps its own PositionState attribute beside the
+    set's compiles (smart.py compiled(): attribute states of a type the sets
+    already hold are the same component kind)."""
+    from abmarl_amd.examples import TeamBattleSim
+    from abmarl_amd.sim.gridworld.components import PositionState
+    from tests.cases import Fighter
+
+    class TwinSim(TeamBattleSim):
+        def __init__(self, **kwargs):
+            super().__init__(**kwargs)
+            self.position_twin = PositionState(**kwargs)
+
+    agents = {f'a{i}': Fighter(id=f'a{i}', encoding=1 + i % 2, move_range=1, attack_range=1,
+                               attack_strength=1, attack_accuracy=1, view_range=2) for i in range(4)}
+    TwinSim.build_sim(5, 5, agents=agents, attack_mapping={1: {2}, 2: {1}},
+                      states={'PositionState', 'HealthState'}, observers={'PositionCenteredEncodingObserver'},
+                      dones={'OneTeamRemainingDone'}).compiled()

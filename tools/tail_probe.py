@@ -114,11 +114,17 @@ def main():
             print(f'    env {i:5d}: {dur[i]:7.1f} us, start +{(start[i] - start.min()) / RT_HZ * 1e6:6.1f}, '
                   f'acting {acting[i]}, steps0 {steps0[i]}, xcc {x[i]} se {se[i]} cu {cu[i]} simd {simd[i]} '
                   f'wave {wave_id[i]}')
-        # block -> CU placement: which env ids share a CU
+        # block -> CU placement: which env ids share a CU, and their SIMDs
         if rep == 0:
             for j in range(2):
-                m = cinv == j
-                print(f'  CU #{j} holds envs {np.nonzero(m)[0][:16].tolist()}')
+                m = np.nonzero(cinv == j)[0]
+                print(f'  CU #{j} holds envs {m[:16].tolist()} on SIMDs {simd[m][:16].tolist()} '
+                      f'(wave ids {wave_id[m][:16].tolist()})')
+        # horizon resets per SIMD: a SIMD with several heavy envs ends last
+        hz = np.bincount(inv, weights=resets.astype(np.float64)).astype(int)
+        print(f'  SIMDs by envs reaching the horizon in the fragment: {np.bincount(hz).tolist()} (index = count); '
+              f'last end by that count: ' + ', '.join(f'{c}: {np.median(last[hz == c]):.1f}'
+                                                      for c in range(hz.max() + 1) if (hz == c).any()))
 
 
 if __name__ == '__main__':
