@@ -175,6 +175,7 @@ struct Params {
     // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
     int32_t obs_lo, obs_hi;                // lanes [obs_lo, obs_hi) hold every grid observer
+    int32_t env_swz;                       // one-wave step kernel: env of workgroup b (block_env)
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
     int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
     int32_t persistent_obs;                // gw_config.persistent_obs: skip rows already -2
@@ -210,6 +211,16 @@ struct Params {
     const int32_t* sblk;                   // static blocking entities: (row << 16) | col
     int32_t n_sblk;
 };
+
+// The env a one-wave step kernel's workgroup b runs: with env_swz = Q > 1
+// (E divisible by Q) workgroup b takes env (b % Q) * (E / Q) + b / Q, so
+// consecutive workgroups -- which the dispatcher places on one CU's SIMDs --
+// hold envs E / Q apart, i.e. at different phases of the bench's staggered
+// episodes; otherwise env b.
+__host__ __device__ inline int block_env(int b, int E, int Q)
+{
+    return (Q > 1 && E % Q == 0) ? (b % Q) * (E / Q) + b / Q : b;
+}
 
 __host__ __device__ inline int mask_words(int r)
 {
@@ -1797,8 +1808,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const int nrand = __popcll(rm);
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps) {
-            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 40] = (uint64_t)rng.pos;
-            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 41] = (uint64_t)nrand;
+            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 40] = (uint64_t)rng.pos;
+            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 41] = (uint64_t)nrand;
         }
 #endif
         if (rng.pos + 2 * nrand <= 2 * GW_MT_N) {
@@ -1864,7 +1875,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)NF : 0u;
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         // randomize_placement_order: the shuffled agents dict's order
-        const int32_t* order = p.place_order ? p.place_order + (size_t)blockIdx.x * A : nullptr;
+        const int32_t* order = p.place_order ? p.place_order + (size_t)block_env(blockIdx.x, p.E, p.env_swz) * A : nullptr;
         for (int pass = 0; pass < 2; pass++) {
             for (int k = 0; k < A; k++) {
                 const int a = order ? (int)uni(order[k]) : k;
@@ -1919,7 +1930,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         if (L.in_grid) { const int gc = to_cell(cell_l); L.r = gc / p.W; L.c = gc % p.W; }
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps)
-            for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 16 + k] = acc_t[k];
+            for (int k = 0; k < 4; k++) p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 16 + k] = acc_t[k];
 #endif
         return true;
     };
@@ -2176,8 +2187,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         ACC_T(4, t0);
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps) {
-            for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
-            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 25] = nsw;
+            for (int k = 0; k < 5; k++) p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
+            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 25] = nsw;
         }
 #endif
         return 0;
@@ -2191,7 +2202,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         return r == 0;
     };
 #ifdef GW_STAMPS
-    const int e = blockIdx.x;
+    const int e = block_env(blockIdx.x, p.E, p.env_swz);
 #endif
     bool ok = true;
     if (what == 1) {
@@ -2290,8 +2301,8 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     constexpr bool PLAIN = SPEC == 1;
     const int sim_kind = PLAIN ? (int)GW_SIM_TEAM_BATTLE : p.sim_kind;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int e = blockIdx.x;
-    if (e >= p.E) return;
+    if ((int)blockIdx.x >= p.E) return;
+    const int e = block_env(blockIdx.x, p.E, p.env_swz);
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
@@ -2854,8 +2865,8 @@ template <int S>
 __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
 {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int e = blockIdx.x;
-    if (e >= p.E) return;
+    if ((int)blockIdx.x >= p.E) return;
+    const int e = block_env(blockIdx.x, p.E, p.env_swz);   // do_reset's env map
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
@@ -2993,8 +3004,8 @@ template <int S>
 __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
 {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int e = blockIdx.x;
-    if (e >= p.E) return;
+    if ((int)blockIdx.x >= p.E) return;
+    const int e = block_env(blockIdx.x, p.E, p.env_swz);   // do_reset's env map
     // reset everything when no selector is given; otherwise the union of the
     // explicit mask, the previous step's __all__ and the horizon
     bool go;
@@ -3916,6 +3927,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
     bool any_ammo = false;
     for (int l = 0; l < A; l++) any_ammo |= (hs[l].kind & GW_K_AMMO) != 0;
+    {
+        const char* swz = getenv("GW_ENV_SWZ");      // A/B of the one-wave env map (tools/tail_probe.py)
+        p.env_swz = swz ? atoi(swz) : 0;
+    }
     g->step_tb = GW_STEP_SPEC && !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
                  !p.hetero_view && !any_ammo;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));

@@ -599,13 +599,19 @@ class UserTeamBattle(SmartGridWorldSimulation):
         self.attack_actor = BinaryAttackActor(**kwargs)
         self.finalize()
 
+    # the len_fix fixtures (tb_ammo_multi, tb_ammo_stacked) ran the example
+    # with `len(attacked) == 0` as its failed-attack test; the reference's
+    # `not attacked` raises ValueError on BinaryAttackActor's numpy array of
+    # 2 or more agents, which the component API returns as such
+    len_fix = False
+
     def step(self, action_dict, **kwargs):
         for agent_id, action in action_dict.items():
             agent = self.agents[agent_id]
             if agent.active:
                 status, attacked = self.attack_actor.process_action(agent, action, **kwargs)
                 if status:
-                    if not attacked:
+                    if (len(attacked) == 0) if self.len_fix else not attacked:
                         self.rewards[agent_id] -= 0.1
                     else:
                         for other in attacked:
@@ -632,7 +638,8 @@ def _obs_array(obs, ids, S):
 
 USER_CASES = [('tb_small', 40, 3), ('tb_order', 30, 2), ('tb_walls', 30, 2),
               ('tb_destroy', 30, 2), ('tb_chase', 30, 2), ('tb_views', 25, 2),
-              ('tb_ammo', 50, 2), ('tb_ammo_multi', 50, 2)]
+              ('tb_ammo', 50, 2), ('tb_ammo_multi', 50, 2), ('tb_value_error', 60, 3),
+              ('tb_value_error_ammo', 40, 2), ('tb_ammo_negative', 40, 2)]
 
 
 @gpu
@@ -646,6 +653,7 @@ def test_user_step_replays_reference(name, steps, envs):
     S = g['obs0'].shape[-1]
     for e in range(envs):
         sim = build_sim(c, sim_cls=UserTeamBattle)
+        sim.len_fix = bool(c.get('len_fix'))
         assert sim._engine_program is None
         m = AllStepManager(sim)
         ids = list(m.agents)
@@ -656,8 +664,20 @@ def test_user_step_replays_reference(name, steps, envs):
             acts = {aid: {'move': g['actions'][t, e, i, :2].astype(int),
                           'attack': int(g['actions'][t, e, i, 2])}
                     for i, aid in enumerate(ids) if aid not in m.done_agents}
-            obs, rew, done, _ = m.step(acts)
             where = f'{name} env {e} step {t}'
+            if 'err' in g and g['err'][t, e]:
+                # the reference's step raised ValueError (team_battle_example.py:41)
+                with pytest.raises(ValueError):
+                    m.step(acts)
+                st = np.random.get_state()
+                assert st[2] == g['mt_pos'][t, e], where
+                assert zlib.crc32(np.ascontiguousarray(st[1], dtype=np.uint32).tobytes()) == \
+                    int(g['mt_crc'][t, e]), where
+                obs = m.reset()
+                np.testing.assert_array_equal(_obs_array(obs, ids, S), g['reset_obs'][t, e],
+                                              err_msg=where + ' reset')
+                continue
+            obs, rew, done, _ = m.step(acts)
             np.testing.assert_array_equal(_obs_array(obs, ids, S), g['obs'][t, e], err_msg=where)
             for i, aid in enumerate(ids):
                 if aid in rew:
