@@ -219,6 +219,7 @@ struct Params {
 // episodes; otherwise env b.
 __host__ __device__ inline int block_env(int b, int E, int Q)
 {
+    if (Q == -1) return E - 1 - b;                  // reversed
     return (Q > 1 && E % Q == 0) ? (b % Q) * (E / Q) + b / Q : b;
 }
 
