@@ -175,7 +175,6 @@ struct Params {
     // ReachTheTarget on a workgroup per env (gw_rtt.inc)
     int32_t nwv;                           // waves per env (blockDim = 64 * nwv)
     int32_t obs_lo, obs_hi;                // lanes [obs_lo, obs_hi) hold every grid observer
-    int32_t env_swz;                       // one-wave step kernel: env of workgroup b (block_env)
     int32_t par_moves;                     // no Grid.query can refuse a mover: parallel move pass
     int32_t place_par;                     // placement without duplicate removals: parallel (Jacobi)
     int32_t persistent_obs;                // gw_config.persistent_obs: skip rows already -2
@@ -211,17 +210,6 @@ struct Params {
     const int32_t* sblk;                   // static blocking entities: (row << 16) | col
     int32_t n_sblk;
 };
-
-// The env a one-wave step kernel's workgroup b runs: with env_swz = Q > 1
-// (E divisible by Q) workgroup b takes env (b % Q) * (E / Q) + b / Q, so
-// consecutive workgroups -- which the dispatcher places on one CU's SIMDs --
-// hold envs E / Q apart, i.e. at different phases of the bench's staggered
-// episodes; otherwise env b.
-__host__ __device__ inline int block_env(int b, int E, int Q)
-{
-    if (Q == -1) return E - 1 - b;                  // reversed
-    return (Q > 1 && E % Q == 0) ? (b % Q) * (E / Q) + b / Q : b;
-}
 
 __host__ __device__ inline int mask_words(int r)
 {
@@ -1809,8 +1797,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         const int nrand = __popcll(rm);
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps) {
-            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 40] = (uint64_t)rng.pos;
-            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 41] = (uint64_t)nrand;
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 40] = (uint64_t)rng.pos;
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 41] = (uint64_t)nrand;
         }
 #endif
         if (rng.pos + 2 * nrand <= 2 * GW_MT_N) {
@@ -1876,7 +1864,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         uint32_t lens = (l >= 1 && l <= p.max_enc) ? (uint32_t)NF : 0u;
         const uint32_t all_encs = ((2u << p.max_enc) - 1u) & ~1u;
         // randomize_placement_order: the shuffled agents dict's order
-        const int32_t* order = p.place_order ? p.place_order + (size_t)block_env(blockIdx.x, p.E, p.env_swz) * A : nullptr;
+        const int32_t* order = p.place_order ? p.place_order + (size_t)blockIdx.x * A : nullptr;
         for (int pass = 0; pass < 2; pass++) {
             for (int k = 0; k < A; k++) {
                 const int a = order ? (int)uni(order[k]) : k;
@@ -1931,7 +1919,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         if (L.in_grid) { const int gc = to_cell(cell_l); L.r = gc / p.W; L.c = gc % p.W; }
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps)
-            for (int k = 0; k < 4; k++) p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 16 + k] = acc_t[k];
+            for (int k = 0; k < 4; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 16 + k] = acc_t[k];
 #endif
         return true;
     };
@@ -2037,6 +2025,84 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             wave_sync();
         }
         ACC_T(0, t0);
+        // interval(n - 1) draws: stream offsets = exclusive scan of words
+        // used; iterate until consistent (each pass fixes the first lane)
+        auto draw_all = [&](uint32_t n, int& used, int& nidx, bool& bad_) {
+            const bool draws = rnd && n > 1;
+            const uint32_t mx = n - 1u;
+            uint32_t mk = mx;
+            mk |= mk >> 1; mk |= mk >> 2; mk |= mk >> 4; mk |= mk >> 8; mk |= mk >> 16;
+            for (int it = 0; it <= WAVE; it++) {
+                const int st = (int)(wave_incl_scan((uint32_t)used) - (uint32_t)used);
+                int nu = 0;
+                nidx = 0;
+                bad_ = false;
+                if (draws) {
+                    int q = st;
+                    for (;;) {
+                        if (q >= JAC_WB) { bad_ = true; break; }
+                        const uint32_t w = wbuf[CIDX(q, JAC_WB, 13)] & mk;
+                        q++;
+                        if (w <= mx) { nidx = (int)w; break; }
+                    }
+                    nu = q - st;
+                }
+                const bool ch = __ballot(nu != used) != 0;
+                used = nu;
+                if (!ch) break;
+            }
+        };
+        // every cell placed leaves every list (no initial positions, no
+        // overlap at reset, every encoding listed): one shared list, |list|
+        // = NF - #placed before, and the cells are the decoded Lehmer code of
+        // the draws -- backwards over the lanes, each later lane's rank moves
+        // past the cell of the lane before it (the rank of c_j among the cells
+        // c_j, ..., c_k is fixed once the lanes after j are decoded).  No
+        // ranking tables, no sweeps: one readlane + compare per placed lane.
+        const bool shared = !valid || (rnd && rem == all_encs && ((all_encs >> L.enc) & 1u));
+        if (nrnd > 0 && __ballot(!shared) == 0) {
+            const uint32_t n = (uint32_t)NF - (uint32_t)__popcll(rndm & lt_l);
+            if (__ballot(rnd && n == 0)) return 2;   // the serial loop raises at the right point
+            int used = rnd ? 1 : 0, nidx = 0;
+            bool bad_ = false;
+            draw_all(n, used, nidx, bad_);
+            if (__ballot(bad_)) return 2;
+            ACC_T(2, t0);
+            int v = nidx;
+            for (uint64_t m = rndm & ~(1ull << (63 - __builtin_clzll(rndm))); m;) {
+                const int j = 63 - __builtin_clzll(m);
+                m &= ~(1ull << j);
+                const int vj = rl(v, j);
+                if (rnd && l > j && v >= vj) v++;
+            }
+            ACC_T(3, t0);
+            const int total = (int)rl(wave_incl_scan((uint32_t)used), WAVE - 1);
+            const int np = pos0 + total;
+            if (np > GW_MT_N) {
+                mt_twist_call(rng.key);
+                rng.pos = np - GW_MT_N;
+                rng.dirty = true;
+            } else {
+                rng.pos = np;
+            }
+            rng.base = -1;
+            CHECK(!valid || (v >= 0 && v < NF), 7, v, l);
+            if (valid) {
+                L.in_grid = true;
+                const int gc = to_cell(v);
+                L.r = gc / p.W; L.c = gc % p.W;
+                L.seq = (uint32_t)__popcll(rndm & lt_l);
+            }
+            ctr = (uint32_t)nrnd;
+            ACC_T(4, t0);
+#ifdef GW_STAMPS
+            if (l == 0 && p.stamps) {
+                for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
+                p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 25] = 0;
+            }
+#endif
+            return 0;
+        }
         auto lanes_upto = [&](uint32_t r) -> uint64_t {   // lanes of the r lowest cells
             if (r == 0) return 0ull;
             const uint2 t = tb[CIDX((int)r - 1, WAVE, 16)];
@@ -2059,32 +2125,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             const uint64_t rm = mym & before;
             n = (uint32_t)NF - (uint32_t)__popcll(rm);
             ACC_T(1, t0);
-            // interval(n - 1) draws: stream offsets = exclusive scan of words
-            // used; iterate until consistent (each pass fixes the first lane)
-            const bool draws = rnd && n > 1;
-            const uint32_t mx = n - 1u;
-            uint32_t mk = mx;
-            mk |= mk >> 1; mk |= mk >> 2; mk |= mk >> 4; mk |= mk >> 8; mk |= mk >> 16;
             int nidx = 0;
-            for (int it = 0; it <= WAVE; it++) {
-                const int st = (int)(wave_incl_scan((uint32_t)used) - (uint32_t)used);
-                int nu = 0;
-                nidx = 0;
-                bad = false;
-                if (draws) {
-                    int q = st;
-                    for (;;) {
-                        if (q >= JAC_WB) { bad = true; break; }
-                        const uint32_t w = wbuf[CIDX(q, JAC_WB, 13)] & mk;
-                        q++;
-                        if (w <= mx) { nidx = (int)w; break; }
-                    }
-                    nu = q - st;
-                }
-                const bool ch = __ballot(nu != used) != 0;
-                used = nu;
-                if (!ch) break;
-            }
+            draw_all(n, used, nidx, bad);
             ACC_T(2, t0);
             // rank this sweep's cell estimates
             // a new draw starts from its expected cell, the idx-th of n listed
@@ -2188,8 +2230,8 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         ACC_T(4, t0);
 #ifdef GW_STAMPS
         if (l == 0 && p.stamps) {
-            for (int k = 0; k < 5; k++) p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
-            p.stamps[(size_t)block_env(blockIdx.x, p.E, p.env_swz) * GW_STAMP_STRIDE + 25] = nsw;
+            for (int k = 0; k < 5; k++) p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 20 + k] = acc_t[k];
+            p.stamps[(size_t)blockIdx.x * GW_STAMP_STRIDE + 25] = nsw;
         }
 #endif
         return 0;
@@ -2203,7 +2245,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         return r == 0;
     };
 #ifdef GW_STAMPS
-    const int e = block_env(blockIdx.x, p.E, p.env_swz);
+    const int e = blockIdx.x;
 #endif
     bool ok = true;
     if (what == 1) {
@@ -2303,7 +2345,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     const int sim_kind = PLAIN ? (int)GW_SIM_TEAM_BATTLE : p.sim_kind;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     if ((int)blockIdx.x >= p.E) return;
-    const int e = block_env(blockIdx.x, p.E, p.env_swz);
+    const int e = blockIdx.x;
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
@@ -2867,7 +2909,7 @@ __global__ __launch_bounds__(WAVE) void comp_kernel(Params p)
 {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     if ((int)blockIdx.x >= p.E) return;
-    const int e = block_env(blockIdx.x, p.E, p.env_swz);   // do_reset's env map
+    const int e = blockIdx.x;
     const int l = lane_id();
     const int A = p.A;
     const bool valid = l < A;
@@ -3006,7 +3048,7 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Params p)
 {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     if ((int)blockIdx.x >= p.E) return;
-    const int e = block_env(blockIdx.x, p.E, p.env_swz);   // do_reset's env map
+    const int e = blockIdx.x;
     // reset everything when no selector is given; otherwise the union of the
     // explicit mask, the previous step's __all__ and the horizon
     bool go;
@@ -3928,10 +3970,6 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
     bool any_ammo = false;
     for (int l = 0; l < A; l++) any_ammo |= (hs[l].kind & GW_K_AMMO) != 0;
-    {
-        const char* swz = getenv("GW_ENV_SWZ");      // A/B of the one-wave env map (tools/tail_probe.py)
-        p.env_swz = swz ? atoi(swz) : 0;
-    }
     g->step_tb = GW_STEP_SPEC && !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
                  !p.hetero_view && !any_ammo;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));

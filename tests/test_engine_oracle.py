@@ -95,6 +95,21 @@ def test_dense_configs(oracle_mod, kw):
 
 
 @pytest.mark.parametrize('kw', [
+    dict(overlap={}),
+    dict(no_overlap_at_reset=True),
+    dict(rows=8, cols=8, n_agents=60, n_teams=3, overlap={}),   # 4 cells left for the last
+    dict(rows=6, cols=11, n_agents=64, n_teams=4, no_overlap_at_reset=True),
+])
+def test_shared_list_placement(oracle_mod, kw):
+    """Every placed cell leaves every list (no overlapping, or
+    no_overlap_at_reset): the placement decodes the draws as a Lehmer code
+    (gw_engine.hip do_reset, `shared`) -- against the oracle's sequential
+    PositionState.reset, resets every few steps."""
+    cc = team_battle(**kw)
+    _run(oracle_mod, cc, E=1024, T=60, horizon=7, seed_run=14, key=31, check_every=1)
+
+
+@pytest.mark.parametrize('kw', [
     # 128 BattleAgents on 32x32 (the headline grid with twice the fighters)
     dict(rows=32, cols=32, n_agents=128, n_teams=2),
     # 200 fighters, 4 teams, accuracy < 1, stacked double attacks, range 2

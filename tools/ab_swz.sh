@@ -1,6 +1,8 @@
 #!/bin/bash
 # A/B of the one-wave step kernel's env map (block_env, GW_ENV_SWZ = Q) on the
 # driver's headline command, alternating, 3 rounds; then the tail probe per Q.
+# (Round 5; the knob was removed after the A/B, profiles/r05/ab_env_map/: the
+# identity map stayed.)
 #   bash tools/ab_swz.sh "0 4 16" -> gpurun_out/ab_swz.jsonl, gpurun_out/ab_swz_tail_<Q>.log
 set -o pipefail
 QS=${1:-"0 4 16"}
