@@ -163,7 +163,7 @@ struct Params {
     double prw[5];                         // bad_move, entropy, eat_food, kill, die
     int32_t n_passive, pwords;             // passive entities (food), bit words per env
     const int16_t* passive_cell;           // [n_passive] cell
-    const int16_t* cell_passive;           // [HW] passive index, -1 = none
+    const int16_t* cell_passive;           // [HW] passive index | encoding << 8, -1 = none
     const uint32_t* passive_cnt;           // [ceil(HW/4)] packed u8: passive entities per cell
     const int8_t* passive_enc;             // [n_passive]
     uint32_t* pbits;                       // [E][pwords] passive present
@@ -3577,6 +3577,21 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
         set_err("%d food entities > %d", (int)passive.size(), 32 * PAC_MAX_PWORDS);
         return GW_E_UNSUPPORTED;
     }
+    {
+        // the cell -> food map holds one food per cell (food_at, pac_tables)
+        std::vector<uint8_t> has_food(HW, 0);
+        for (int a : passive) {
+            if (cfg->agents[a].encoding < 0 || cfg->agents[a].encoding > 127) {   // packed with its index
+                set_err("food entity %d: encoding %d outside [0, 127]", a, cfg->agents[a].encoding);
+                return GW_E_UNSUPPORTED;
+            }
+            const int cell = cfg->agents[a].init_row * cfg->cols + cfg->agents[a].init_col;
+            if (cell < 0 || cell >= HW || has_food[cell]++) {
+                set_err("food entity %d: its cell is off the grid or holds another food", a);
+                return GW_E_UNSUPPORTED;
+            }
+        }
+    }
     std::vector<uint8_t> is_static(HW, 0);
     for (int a : statics) {
         const int cell = cfg->agents[a].init_row * cfg->cols + cfg->agents[a].init_col;
@@ -3858,9 +3873,10 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     p.pair_cap = (int)((work_bytes(HW, A, Sst, max_enc) - (size_t)A * Sst * ((Sst + 3) & ~3)) / 2);
     g->smem_step = smem_bytes(HW, A, Sst, max_enc, p.tbl_rows * p.pitch);
     if (pac) {
-        // pac_carve: cval | pb | clist | cp | penc
-        const size_t pw = align16((size_t)HW) + align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
-                          align16(2 * (size_t)HW) + 32 * PAC_MAX_PWORDS + 64 * PAC_MAX_PWORDS;
+        // pac_carve: pb | clist | cp | pcell | ob
+        const size_t pw = align16(4 * PAC_MAX_PWORDS) + 4 * WAVE +
+                          align16(2 * (size_t)HW) + 64 * PAC_MAX_PWORDS +
+                          align16((size_t)HW);
         // the Pacman program never places by draws (every entity starts at its
         // initial position): no placement scratch in its work area, so more
         // envs share a CU (8.2 KB -> 5.4 KB per env at pacman.txt's 21x21)
@@ -3935,7 +3951,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             const gw_agent_spec& s = cfg->agents[passive[k]];
             const int cell = s.init_row * cfg->cols + s.init_col;
             pc[k] = (int16_t)cell;
-            pc[n8 + cell] = (int16_t)k;
+            pc[n8 + cell] = (int16_t)(k | (s.encoding << 8));   // food_at: index and encoding
             cnt[cell >> 2] += 1u << (8 * (cell & 3));
             pe[k] = (int8_t)s.encoding;
         }

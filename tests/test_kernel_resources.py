@@ -143,22 +143,70 @@ def twist_memory_ops(path):
     return found
 
 
-@pytest.mark.parametrize('variant', ['', 'checks'])
-def test_mt_key_never_read_through_flat(variant):
-    """Every MT19937 twist in every kernel reads the key with ds_* operations:
-    the key pointer is LDS-typed (lds_u32) everywhere.  A generic key pointer
-    in a scratch-resident Rng (the generic-window kernels, the checks build)
-    made LLVM read the key[i] / key[i + 1] pair as ONE flat_load_dwordx2 at
-    key + 4i -- a 64-bit LDS access off its natural alignment for odd i, the
-    round-4 memory aperture violation (DESIGN §4 "MT19937 key addressing")."""
+def flat_functions(path):
+    """({function: number of flat_* instructions}, {functions that form a
+    generic LDS address: src_shared_base}) of the library's gfx950 code."""
+    import subprocess
+    import tempfile
+    flat, shared = {}, set()
+    for co in code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix='.co') as f:
+            f.write(co)
+            f.flush()
+            txt = subprocess.run([OBJDUMP, '-d', '--mcpu=gfx950', f.name], check=True,
+                                 capture_output=True, text=True).stdout.split('\n')
+        fn = None
+        for ln in txt:
+            m = re.match(r'^[0-9a-f]+ <(.+)>:', ln)
+            if m:
+                fn = m.group(1)
+            elif ln.strip().startswith('flat_'):
+                flat[fn] = flat.get(fn, 0) + 1
+            if 'src_shared_base' in ln:
+                shared.add(fn)
+    return flat, shared
+
+
+def _lib(variant):
     from abmarl_amd import _native
     path = _native.variant_lib(variant)
     if not os.path.exists(path):
         pytest.skip(f'{os.path.basename(path)} not built')
     if not os.path.exists(OBJDUMP):
         pytest.skip('llvm-objdump missing')
-    ops = twist_memory_ops(path)
+    return path
+
+
+@pytest.mark.parametrize('variant', ['', 'checks'])
+def test_mt_key_never_read_through_flat(variant):
+    """Every MT19937 twist in every kernel reads the key with ds_* operations:
+    the key pointer is LDS-typed (lds_u32) everywhere.  The round-4 memory
+    aperture violation: a generic key pointer, held in a scratch-resident Rng
+    (the generic-window kernels), made the inlined twist flat_* accesses, and
+    LLVM folded part of the key[i - 227] index into the instruction's
+    immediate offset -- `flat_load_dword v, v[a:b] offset:768` with the VGPR
+    address key + 4 * lane - 908, below the LDS aperture base (the key is at
+    LDS offset 0), which selects no aperture (DESIGN §4 "MT19937 key
+    addressing", tools/fault_r05/)."""
+    ops = twist_memory_ops(_lib(variant))
     assert ops, 'no twist found in the library'
     bad = {fn: sorted(o) for fn, o in ops.items() if any(x.startswith('flat_') for x in o)}
     assert not bad, bad
     assert all(any(x.startswith('ds_') for x in o) for o in ops.values()), ops
+
+
+@pytest.mark.parametrize('variant', ['', 'checks'])
+def test_no_generic_lds_pointer(variant):
+    """No kernel forms a generic (flat) address of LDS -- src_shared_base,
+    the LDS aperture, appears nowhere -- so no flat_* instruction can reach
+    LDS, and no folded immediate offset can push a flat LDS address out of
+    its aperture (the round-4 fault, which 95ec8c4's reset_kernel<0> shows
+    with its two src_shared_base materialisations of the key pointer).  The
+    production step / reset / rollout kernels have no flat_* instruction at
+    all; the component-API kernels and the checks build keep flat loads of
+    the global arrays behind a Params copy in scratch."""
+    flat, shared = flat_functions(_lib(variant))
+    assert not shared, sorted(shared)
+    if variant == '':
+        bad = {fn: n for fn, n in flat.items() if 'comp_kernel' not in fn}
+        assert not bad, bad
