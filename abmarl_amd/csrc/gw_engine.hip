@@ -138,6 +138,7 @@ struct Params {
     int32_t act_dim;                       // ints per entity action (gw_config_act_dim)
     int32_t attack_kind;                   // GW_ATTACK_*
     const uint4* tbl_tmpl;                 // empty padded table (0xFF border), 16-B granules
+    const uint4* ob_tmpl;                  // the same unpadded, row-major [H][W] (Pacman's copy)
     uint32_t overlap[GW_MAX_ENC + 1];
     uint32_t amap[GW_MAX_ENC + 1];
     // static entities (gw_engine.h "Entities and lanes") and blocking
@@ -3734,9 +3735,15 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             const gw_agent_spec& s = cfg->agents[a];
             ht[(size_t)(s.init_row + pad) * p.pitch + (s.init_col + pad)] = (uint8_t)s.encoding;
         }
-        HIPCHK(hipMalloc(&g->d_tmpl, tb));
-        HIPCHK(hipMemcpy(g->d_tmpl, ht.data(), tb, hipMemcpyHostToDevice));
+        // + the unpadded copy (pac_kernel keeps one beside the table)
+        ht.resize(tb + align16((size_t)HW), 0);
+        for (int r = 0; r < cfg->rows; r++)
+            for (int c = 0; c < cfg->cols; c++)
+                ht[tb + (size_t)r * cfg->cols + c] = ht[(size_t)(r + pad) * p.pitch + (c + pad)];
+        HIPCHK(hipMalloc(&g->d_tmpl, ht.size()));
+        HIPCHK(hipMemcpy(g->d_tmpl, ht.data(), ht.size(), hipMemcpyHostToDevice));
         p.tbl_tmpl = g->d_tmpl;
+        p.ob_tmpl = (const uint4*)((const uint8_t*)g->d_tmpl + tb);
     }
     // free cells (PositionState lists never hold a static cell: every list
     // loses it when the static entity is placed, before any draw)
