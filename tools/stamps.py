@@ -80,6 +80,14 @@ def main():
     st = eng.stamps.cpu().numpy()
     if wl == 'rtt':
         report(st, list(range(10)), STEP, f'{wl}: step launch {NSTEPS} (next_step auto-reset)')
+        if (st[:, 35] != 0).any():
+            report(st, [5, 30, 31, 32, 35], {30: 'crowd: members ranked', 31: 'crowd: pairs + words',
+                                             32: 'crowd: offset scans', 35: 'crowd: values'},
+                   'crowded draws, parallel form')
+            ok = st[:, 35] != 0
+            print(f'{"pairs":>24}: median {np.median(st[ok, 33]):.0f} max {st[ok, 33].max()}; members median '
+                  f'{np.median(st[ok, 34]):.0f} max {st[ok, 34].max()}; scan passes median '
+                  f'{np.median(st[ok, 36]):.0f} max {st[ok, 36].max()}')
         tot = st[:, 9] - st[:, 0]
     else:
         stepped = st[:, 2] != 0
