@@ -2115,19 +2115,27 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
         int idx = rnd ? -1 : 0;
         uint32_t n = 0;
         bool bad = false, qbad = false;
+        // the list lengths and the draws depend on the other lanes' fresh
+        // sets only: a sweep that changed no fresh set leaves them as they are
+        // (after the first sweep only a shared cell changes one)
+        uint64_t rm = 0;
+        bool fresh_dirty = true;
         for (int sweep = 0;; sweep++) {
             if (sweep == MAX_SWEEPS) return 2;
-            // |list enc| when this lane is placed, and who shortened it
-            uint64_t mym = 0;
-            for (int f = 1; f <= p.max_enc; f++) {
-                const uint64_t m = __ballot((fresh >> f) & 1u);
-                if (L.enc == f) mym = m;
+            int nidx = idx;
+            if (fresh_dirty) {
+                // |list enc| when this lane is placed, and who shortened it
+                uint64_t mym = 0;
+                for (int f = 1; f <= p.max_enc; f++) {
+                    const uint64_t m = __ballot((fresh >> f) & 1u);
+                    if (L.enc == f) mym = m;
+                }
+                rm = mym & before;
+                n = (uint32_t)NF - (uint32_t)__popcll(rm);
+                ACC_T(1, t0);
+                nidx = 0;
+                draw_all(n, used, nidx, bad);
             }
-            const uint64_t rm = mym & before;
-            n = (uint32_t)NF - (uint32_t)__popcll(rm);
-            ACC_T(1, t0);
-            int nidx = 0;
-            draw_all(n, used, nidx, bad);
             ACC_T(2, t0);
             // rank this sweep's cell estimates
             // a new draw starts from its expected cell, the idx-th of n listed
@@ -2200,6 +2208,7 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             const uint32_t nf = rem & ~dup;
             const bool lane_ch = valid && (ovf || c != ce0 || nf != fresh || nidx != idx);
             const bool any = __ballot(lane_ch) != 0;
+            fresh_dirty = __ballot(valid && nf != fresh) != 0;
             cell = c; fresh = nf; idx = nidx; qbad = qb;
             ACC_T(3, t0);
 #ifdef GW_STAMPS
