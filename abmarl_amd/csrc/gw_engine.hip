@@ -2441,6 +2441,8 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
         // this step's actions (step 0's came with the prologue); loading the
         // next step's ahead and parking them in LDS measured 2 % slower per
         // 100-step fragment (profiles/r03/ab_head_prefetch.jsonl)
+        // (a step ahead in registers, round 5: neutral on the driver's command
+        // and 100-step fragments, profiles/r05/ab_act_ahead_dropped_*.jsonl)
         if (t > 0) {
             const int32_t* ap = act_t + act_row;
             const int a0 = ap[0], a1 = ap[1], a2 = ap[2];

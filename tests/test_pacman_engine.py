@@ -369,3 +369,25 @@ def test_allstep_rollout_matches_steps(mode):
             assert (out['obs'][s].cpu().numpy() == obs.cpu().numpy()).all(), f"step {t + s}: obs"
         t += f
     _same_state(a, b)
+
+
+def test_two_foods_on_one_cell_refused():
+    """The Pacman program places every entity at its own initial cell and
+    its cell -> food map holds one food per cell (gw_pacman.inc food_at):
+    gw_create refuses a layout with two foods on a cell."""
+    import numpy as np
+    from abmarl_amd._native import EngineError
+    from abmarl_amd.engine import GridWorldEngine, env_seeds
+    from abmarl_amd.examples.pacman import PacmanSim, PacmanAgent, FoodAgent, BaddieAgent
+    agents = {
+        'pacman': PacmanAgent(id='pacman', encoding=1, initial_position=np.array([0, 0])),
+        'baddie_0': BaddieAgent(id='baddie_0', encoding=4, initial_position=np.array([4, 4])),
+        'food_0': FoodAgent(id='food_0', encoding=3, initial_position=np.array([2, 2])),
+        'food_1': FoodAgent(id='food_1', encoding=3, initial_position=np.array([2, 2])),
+    }
+    sim = PacmanSim.build_sim(5, 5, agents=agents,
+                              states={'PositionState', 'OrientationState', 'HealthState'},
+                              observers={'AbsoluteEncodingObserver'},
+                              overlapping={1: {3, 4}, 3: {3}, 4: {3, 4}})
+    with pytest.raises(EngineError, match='share initial cell|another food'):
+        GridWorldEngine(sim.compiled(), 4, seeds=env_seeds(4))
