@@ -2334,8 +2334,11 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 #ifndef GW_STEP_WAVES_PER_EU
 #define GW_STEP_WAVES_PER_EU 4
 #endif
+// a pending horizon reset counts as this many agent-steps of remaining work
+// (192 -> 384 in round 5: the driver's command median 0.2298 -> 0.2253 ms over
+// 8 alternating runs, 100-step fragments unchanged; profiles/r05/ab_prio_reset_w*.jsonl)
 #ifndef GW_PRIO_RESET_W
-#define GW_PRIO_RESET_W 192
+#define GW_PRIO_RESET_W 384
 #endif
 // lane_step_kernel: steps of actions in flight ahead of the step (gw_lane.inc)
 #ifndef GW_LANE_PD

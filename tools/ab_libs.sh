@@ -7,7 +7,7 @@ OUT=$1; ARMS=$2; shift 2
 ARGS=${*:-"--steps 20 --warmup 5"}
 mkdir -p gpurun_out
 : > gpurun_out/$OUT.jsonl
-for r in 1 2 3; do
+for r in $(seq 1 ${ROUNDS:-3}); do
   for arm in $ARMS; do
     name=${arm%%=*}; lib=${arm#*=}
     if [ "$lib" = "-" ]; then unset GW_ENGINE_LIB; else export GW_ENGINE_LIB=$lib; fi
