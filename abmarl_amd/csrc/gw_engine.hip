@@ -641,6 +641,12 @@ struct Smem {
 // (sized so that the TeamBattle 32x32 env fits 10 KiB of LDS: 16 one-wave
 // envs per CU, all 4096 resident at once on 256 CUs)
 constexpr int JAC_WB = 160;
+// the Jacobi sweeps end without a confirming sweep when at most this many
+// estimates moved in the last one and none of them can change a fixpoint
+// (0: always confirm with a sweep)
+#ifndef GW_JAC_CONFIRM
+#define GW_JAC_CONFIRM 16
+#endif
 static_assert(JAC_WB < GW_MT_N - 397, "placement words past the twist come from the untwisted key");
 constexpr int JAC_OFF_W = 0;
 constexpr int JAC_OFF_PUB = JAC_OFF_W + 4 * JAC_WB;
@@ -2215,6 +2221,32 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             nsw++;
 #endif
             if (!any) break;
+#if GW_JAC_CONFIRM
+            // Would the next sweep change anything?  Each lane's fixpoint of this
+            // sweep is exact against the estimates it ranked (c = idx + #{rm
+            // estimates <= c}, none of them on c), and so is its duplicate set.
+            // With no fresh set changed (same rm, n and draws) they stay exact
+            // against the new estimates unless an estimate that moved crossed c
+            // (an rm lane) or left or landed on c (any earlier lane): then the
+            // confirming sweep is not needed.
+            if (!fresh_dirty && __ballot(ovf) == 0) {
+                const uint64_t mv = __ballot(valid && c != ce0);
+                if (__popcll(mv) <= GW_JAC_CONFIRM) {
+                    bool aff = false;
+                    const uint32_t xy = (uint32_t)ce0 << 16 | (uint32_t)c;   // cells < 2^16
+                    for (uint64_t m = mv; m; m &= m - 1ull) {
+                        const int j = first_lane(m);
+                        const uint32_t xyj = rl(xy, j);
+                        const int x = (int)(xyj >> 16), y = (int)(xyj & 0xffffu);
+                        if ((before >> j) & 1ull) {
+                            aff = aff || x == c || y == c;
+                            if (rnd && ((rm >> j) & 1ull)) aff = aff || ((x < c) != (y < c));
+                        }
+                    }
+                    if (__ballot(valid && aff) == 0) break;
+                }
+            }
+#endif
         }
         if (__ballot(bad)) return 2;
         if (__ballot(ip && qbad)) { err |= GW_ERR_INIT_POSITION; return 1; }   // grid.py:81-129
