@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5 final HEAD: the GPU suite, checks build, smoke, the driver's command,
-# the one-wave values barrier A/B (c2 = before), config 4's rocprof evidence.
+# config 4's rocprof evidence.
 set -o pipefail
 mkdir -p gpurun_out/r05fin4
 export TMPDIR=/tmp
@@ -13,6 +13,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -n1 gpurun_out/r05fin4/smoke.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r05fin4/bench_driver.log 2>&1 || { echo BENCH FAIL; tail -20 gpurun_out/r05fin4/bench_driver.log; exit 1; }
 tail -n1 gpurun_out/r05fin4/bench_driver.log | cut -c1-300
-ROUNDS=3 timeout -k 10 900 bash tools/ab_libs.sh r05fin4/ab_rtt_values "c2=$A/c2/libgw_engine.so new=-" --workload rtt --steps 100 --warmup 5 || exit 1
 timeout -k 10 900 bash tools/prof_headline.sh r05rtt2 rtt > gpurun_out/r05fin4/prof.log 2>&1 || { echo PROF FAIL; tail -20 gpurun_out/r05fin4/prof.log; exit 1; }
 tail -n5 gpurun_out/r05fin4/prof.log
