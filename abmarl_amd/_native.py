@@ -56,6 +56,7 @@ SIGNATURES = {
     'gw_num_lanes': (_i32, [_vp]),
     'gw_env_kernel': (_i32, [_vp]),
     'gw_act_dim': (_i32, [_vp]),
+    'gw_step_occupancy': (_i32, [_vp, _vp, _vp, _vp]),
     'gw_set_placement_order': (_i32, [_vp, _vp, _i32]),
     'gw_set_action_order': (_i32, [_vp, _vp, _i32]),
     'gw_lane_entities': (_i32, [_vp, _vp]),

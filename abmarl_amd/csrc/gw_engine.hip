@@ -2672,7 +2672,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                         ? attack_selective(p, sm, rng, L, a, act_e + (size_t)a * p.act_dim + 2, nlist, list)
                         : attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list, &nd);
                     if (!status) return;
-                    // `not attacked_agents` (reach_the_target.py:107) on a numpy array
+                    // `not attacked_agents` (reach_the_target.py:127) on a numpy array
                     if (nd && nlist >= 2 && !p.arr_as_list) { raised = GW_ERR_VALUE_ERROR; return; }
                     if (nlist == 0) { if (l == a) L.reward -= 0.1; }
                     else {
@@ -3242,12 +3242,14 @@ enum PartKernel { PK_STEP = 0, PK_RESET = 1, PK_WG_STEP = 2, PK_WG_RESET = 3, PK
 typedef hipError_t (*part_launch_fn)(int kind, unsigned grid, unsigned block, size_t smem,
                                      hipStream_t st, const void* params, hipEvent_t ev0, hipEvent_t ev1);
 typedef hipError_t (*part_attr_fn)(int kind, size_t bytes);
+typedef hipError_t (*part_occ_fn)(int kind, unsigned block, size_t smem, int* nblk);
 #define GW_PART_CAT2(a, b) a##b
 #define GW_PART_CAT(a, b) GW_PART_CAT2(a, b)
 #define GW_PART_DECL(S_)                                                                      \
     hipError_t GW_PART_CAT(gw_part_launch_, S_)(int, unsigned, unsigned, size_t, hipStream_t, \
                                                 const void*, hipEvent_t, hipEvent_t);         \
-    hipError_t GW_PART_CAT(gw_part_attr_, S_)(int, size_t);
+    hipError_t GW_PART_CAT(gw_part_attr_, S_)(int, size_t);                                  \
+    hipError_t GW_PART_CAT(gw_part_occ_, S_)(int, unsigned, size_t, int*);
 GW_PART_DECL(1) GW_PART_DECL(3) GW_PART_DECL(5) GW_PART_DECL(7)
 GW_PART_DECL(9) GW_PART_DECL(11) GW_PART_DECL(13) GW_PART_DECL(15)
 GW_PART_DECL(0)   // the generic window path: S at run time (> 2 * GW_FIXED_RANGE + 1)
@@ -3292,27 +3294,43 @@ hipError_t GW_PART_CAT(gw_part_launch_, GW_PART_S)(int kind, unsigned grid, unsi
 #endif
 }
 
-hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
+// the part's kernel for a PartKernel kind (nullptr: not in this part)
+static const void* part_kernel(int kind)
 {
 #if GW_PART_S == 0
-    const void* k0 = kind == PK_STEP ? (const void*)step_kernel<0, 0>
-                   : kind == PK_RESET ? (const void*)reset_kernel<0>
-                   : kind == PK_COMP ? (const void*)comp_kernel<0> : nullptr;
-    if (!k0) return hipErrorInvalidValue;
-    return hipFuncSetAttribute(k0, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    return kind == PK_STEP ? (const void*)step_kernel<0, 0>
+         : kind == PK_RESET ? (const void*)reset_kernel<0>
+         : kind == PK_COMP ? (const void*)comp_kernel<0> : nullptr;
 #else
     constexpr int S = GW_PART_S;
-    const void* k = kind == PK_STEP ? (const void*)step_kernel<S, 0>
-                  : kind == PK_STEP_TB ? (const void*)step_kernel<S, 1>
-                  : kind == PK_RESET ? (const void*)reset_kernel<S>
-                  : kind == PK_WG_STEP ? (const void*)wg_step_kernel<S>
-                  : kind == PK_COMP ? (const void*)comp_kernel<S>
-                  : kind == PK_STEP_LANE ? (const void*)lane_step_kernel<S>
-                  : kind == PK_STEP_LANE_NS ? (const void*)lane_step_kernel<S, LANE_FL_NS>
-                  : kind == PK_WG_COMP ? (const void*)wg_comp_kernel<S>
-                                       : (const void*)wg_reset_kernel<S>;
-    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    switch (kind) {
+    case PK_STEP: return (const void*)step_kernel<S, 0>;
+    case PK_STEP_TB: return (const void*)step_kernel<S, 1>;
+    case PK_RESET: return (const void*)reset_kernel<S>;
+    case PK_WG_STEP: return (const void*)wg_step_kernel<S>;
+    case PK_WG_RESET: return (const void*)wg_reset_kernel<S>;
+    case PK_COMP: return (const void*)comp_kernel<S>;
+    case PK_STEP_LANE: return (const void*)lane_step_kernel<S>;
+    case PK_STEP_LANE_NS: return (const void*)lane_step_kernel<S, LANE_FL_NS>;
+    case PK_WG_COMP: return (const void*)wg_comp_kernel<S>;
+    default: return nullptr;
+    }
 #endif
+}
+
+hipError_t GW_PART_CAT(gw_part_attr_, GW_PART_S)(int kind, size_t bytes)
+{
+    const void* k = part_kernel(kind);
+    if (!k) return hipErrorInvalidValue;
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// resident workgroups per CU of a kind's launch (gw_step_occupancy)
+hipError_t GW_PART_CAT(gw_part_occ_, GW_PART_S)(int kind, unsigned block, size_t smem, int* nblk)
+{
+    const void* k = part_kernel(kind);
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(nblk, k, (int)block, smem);
 }
 #else   // ------------------------------------------------------- host part
 
@@ -3401,6 +3419,9 @@ static const part_launch_fn k_part_launch[9] = {
 static const part_attr_fn k_part_attr[9] = {
     gw_part_attr_1, gw_part_attr_3, gw_part_attr_5, gw_part_attr_7,
     gw_part_attr_9, gw_part_attr_11, gw_part_attr_13, gw_part_attr_15, gw_part_attr_0};
+static const part_occ_fn k_part_occ[9] = {
+    gw_part_occ_1, gw_part_occ_3, gw_part_occ_5, gw_part_occ_7,
+    gw_part_occ_9, gw_part_occ_11, gw_part_occ_13, gw_part_occ_15, gw_part_occ_0};
 constexpr int FIXED_S = 2 * GW_FIXED_RANGE + 1;
 
 static int part_index(int S)
@@ -3467,7 +3488,7 @@ static hipError_t do_reset(const gw_engine* g, Params& p, hipStream_t st)
 
 extern "C" {
 
-int32_t gw_abi_version(void) { return 6; }
+int32_t gw_abi_version(void) { return 7; }
 const char* gw_last_error(void) { return g_err; }
 
 gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_handle* out)
@@ -3506,6 +3527,20 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
             return GW_E_UNSUPPORTED;
         }
         if (s.init_row >= cfg->rows || s.init_col >= cfg->cols) { set_err("agent %d initial position outside the grid", a); return GW_E_INVALID; }
+        // the agent classes' own assertions (agent.py:122-288)
+        if ((s.kind & GW_K_MOVING) && s.move_range < 0) { set_err("agent %d move_range %d", a, s.move_range); return GW_E_INVALID; }
+        if ((s.kind & GW_K_ATTACKING) &&
+            (s.simultaneous_attacks < 0 || !(s.attack_strength >= 0.0 && s.attack_strength <= 1.0) ||
+             !(s.attack_accuracy >= 0.0 && s.attack_accuracy <= 1.0))) {
+            set_err("agent %d attack parameters (simultaneous %d, strength %g, accuracy %g)", a,
+                    s.simultaneous_attacks, s.attack_strength, s.attack_accuracy);
+            return GW_E_INVALID;
+        }
+        if ((s.kind & GW_K_HEALTH) && s.initial_health == s.initial_health && s.initial_health >= 0.0 &&
+            !(s.initial_health > 0.0 && s.initial_health <= 1.0)) {
+            set_err("agent %d initial_health %g outside (0, 1]", a, s.initial_health);
+            return GW_E_INVALID;
+        }
         if (s.encoding > max_enc) max_enc = s.encoding;
     }
     const bool maze = cfg->sim_kind == GW_SIM_MAZE_NAV;
@@ -4106,6 +4141,30 @@ int32_t gw_env_kernel(gw_handle g)
                    : g->lane_envs ? GW_KERNEL_LANE : GW_KERNEL_WAVE;
 }
 int32_t gw_act_dim(gw_handle g) { return g ? g->base.act_dim : 0; }
+
+gw_status gw_step_occupancy(gw_handle g, int32_t* blocks_per_cu, int32_t* block_threads, int64_t* lds_bytes)
+{
+    EvClear ec{g};
+    if (!g || !blocks_per_cu) return GW_E_INVALID;
+    int nblk = 0;
+    unsigned block = WAVE;
+    size_t smem = g->smem_step;
+    if (g->pacman) {
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nblk, (const void*)pac_kernel<PAC_STEP_ALL>,
+                                                            (int)block, smem));
+    } else {
+        const int pi = part_index(g->S);
+        if (pi < 0) return GW_E_INVALID;
+        int kind = g->wg ? PK_WG_STEP : (g->step_tb ? PK_STEP_TB : PK_STEP);
+        if (g->lane_envs) { kind = PK_STEP_LANE_NS; smem = g->smem_lane; }
+        if (g->wg) block = WAVE * g->base.nwv;
+        HIPCHK(k_part_occ[pi](kind, block, smem, &nblk));
+    }
+    *blocks_per_cu = nblk;
+    if (block_threads) *block_threads = (int32_t)block;
+    if (lds_bytes) *lds_bytes = (int64_t)smem;
+    return GW_OK;
+}
 
 gw_status gw_set_action_order(gw_handle g, const int32_t* lane_order, int32_t n)
 {

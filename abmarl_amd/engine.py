@@ -105,6 +105,15 @@ class GridWorldEngine:
                 pass
             self.h = None
 
+    def step_occupancy(self):
+        """(resident workgroups per CU, threads per workgroup, dynamic LDS
+        bytes) of this engine's step launch (gw_step_occupancy)."""
+        nb, bt, lds = C.c_int32(), C.c_int32(), C.c_int64()
+        with torch.cuda.device(self.device):
+            _native.check(self.L.gw_step_occupancy(self.h, C.byref(nb), C.byref(bt), C.byref(lds)),
+                          'gw_step_occupancy')
+        return nb.value, bt.value, lds.value
+
     # ------------------------------------------------------------ control
     def seed(self, seeds):
         s = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32),

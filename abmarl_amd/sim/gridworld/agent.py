@@ -230,6 +230,16 @@ class AmmoAgent(GridWorldAgent):
         self._initial_ammo = value
 
 
+class _AmmoObservingMeta(type):
+    def __instancecheck__(cls, instance):
+        return isinstance(instance, ObservingAgent) and isinstance(instance, AmmoAgent)
+
+
+class AmmoObservingAgent(AmmoAgent, ObservingAgent, metaclass=_AmmoObservingMeta):
+    """agent.py:324-339: what AmmoObserver serves -- any agent that is both
+    an ObservingAgent and an AmmoAgent counts as one (isinstance)."""
+
+
 class OrientationAgent(GridWorldAgent):
     """agent.py:342-373: orientation 1 left, 2 down, 3 right, 4 up;
     initial_orientation None means random at reset (OrientationState)."""

@@ -71,8 +71,14 @@ def agent_spec(agent, program_type=None, food_type=None):
     return s
 
 
-# the component methods a fused program runs as device code
-_DEVICE_METHODS = ('reset', 'process_action', 'get_obs', 'get_done', 'get_all_done')
+# the component methods a fused program (and the component API) runs as
+# device code: the public ones and the reference's protected hooks they call
+# (actor.py:363-417 attack criteria / subset / determination, state.py:116-152
+# placement lists and placement)
+_DEVICE_METHODS = ('reset', 'process_action', 'get_obs', 'get_done', 'get_all_done',
+                   '_basic_criteria', '_subset_attackables', '_determine_attack',
+                   '_build_available_positions', '_update_available_positions',
+                   '_place_initial_position_agent', '_place_variable_position_agent')
 
 
 def _overridden(obj, builtins):
@@ -81,8 +87,9 @@ def _overridden(obj, builtins):
     base = next((b for b in type(obj).__mro__ if b in builtins), None)
     if base is None or type(obj) is base:
         return []
-    return [m for m in _DEVICE_METHODS
-            if hasattr(base, m) and getattr(type(obj), m, None) is not getattr(base, m, None)]
+    # (a hook the built-in does not define here is still the reference's
+    # hook, which the device code implements: defining it is an override)
+    return [m for m in _DEVICE_METHODS if getattr(type(obj), m, None) is not getattr(base, m, None)]
 
 
 def compile_sim(sim, program, states, observers, dones, actors, state_order,
@@ -114,8 +121,10 @@ def compile_sim(sim, program, states, observers, dones, actors, state_order,
         over = _overridden(x, builtins)
         if over:
             raise UnsupportedConfig(f"{type(x).__name__} overrides {', '.join(over)} of a built-in "
-                                    "component: a fused program runs the built-in's device code "
-                                    "(run it through the component API instead)")
+                                    "component: the engine (fused program and component API alike) "
+                                    "runs the built-in's device code.  Write the behaviour as a "
+                                    "component of your own, derived from the base component class "
+                                    "(run on the host by the component runtime)")
     for s in states:
         if isinstance(s, _TargetPlacementState):
             raise UnsupportedConfig(f"{type(s).__name__} runs through the component API "

@@ -16,6 +16,11 @@ from abmarl_amd.sim.gridworld.components import (
     StateBaseComponent, PositionState, MazePlacementState, TargetBarriersFreePlacementState,
     HealthState, OrientationState, AmmoState,
 )
+# off the fused programs: these run on the host (host_components.py)
+from abmarl_amd.sim.gridworld.host_components import (
+    EncodingBasedAttackActor, RestrictedSelectiveAttackActor, StackedPositionCenteredEncodingObserver,
+    AbsolutePositionObserver, AmmoObserver,
+)
 
 _subclass_check_mapping = {
     'actor': ActorBaseComponent,
@@ -25,9 +30,11 @@ _subclass_check_mapping = {
 }
 
 _registered_components = {
-    'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor},
+    'actor': {MoveActor, CrossMoveActor, DriftMoveActor, BinaryAttackActor, SelectiveAttackActor,
+              EncodingBasedAttackActor, RestrictedSelectiveAttackActor},
     'done': {ActiveDone, OneTeamRemainingDone, TargetAgentDone, TargetDestroyedDone},
-    'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver},
+    'observer': {PositionCenteredEncodingObserver, AbsoluteEncodingObserver,
+                 StackedPositionCenteredEncodingObserver, AbsolutePositionObserver, AmmoObserver},
     'state': {PositionState, MazePlacementState, TargetBarriersFreePlacementState, HealthState,
               AmmoState, OrientationState},
 }

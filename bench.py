@@ -34,8 +34,12 @@ wall time over ranks.  The engine counts acting agents on device.
 Usage: python bench.py [--gpus N --steps K --warmup W]
        N > 1 launches N ranks itself (torch.distributed.run, one process per
        GPU, RCCL) unless it already runs under a launcher that set WORLD_SIZE,
-       which must then equal N:
+       which must then equal N (--gpus omitted: N = WORLD_SIZE):
        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+       Readiness runs of the multi-rank path on a one-GPU box only:
+       --share-gpu --dist-backend gloo (every rank on cuda:0; the collectives
+       over gloo on host copies; RCCL refuses two ranks on one GPU).  Such a
+       line is not a scaling measurement.
 """
 import argparse
 import json
@@ -349,6 +353,8 @@ def launch_ranks(n):
     the GPU (torch.cuda.device_count() does not initialise it)."""
     import socket
     import subprocess
+    if torch.cuda.is_initialized():
+        raise RuntimeError('launch_ranks: HIP is already initialised in the launching process')
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
@@ -357,27 +363,49 @@ def launch_ranks(n):
     return subprocess.call(cmd, cwd=ROOT)
 
 
-def check_world(gpus):
+def resolve_gpus(gpus):
+    """--gpus as given, or (omitted) the launcher's WORLD_SIZE, else 1."""
+    if gpus is not None:
+        return gpus
+    return int(os.environ.get('WORLD_SIZE', '1'))
+
+
+def check_world(gpus, share_gpu=False, backend='nccl'):
     """The rank layout --gpus N asks for: None when this process is one of the
-    N ranks (or N == 1), 'launch' when it must start them, else an error."""
+    N ranks (or N == 1), 'launch' when it must start them, else an error.
+    Reads no GPU state (torch.cuda.device_count() does not initialise HIP on
+    this image; tests/test_bench_launch.py checks the launcher leaves it
+    uninitialised)."""
     world = os.environ.get('WORLD_SIZE')
     if gpus < 1:
         return f'--gpus {gpus}: at least one GPU'
+    if share_gpu and gpus > 1 and backend != 'gloo':
+        return '--share-gpu needs --dist-backend gloo (RCCL refuses two ranks on one GPU)'
+    if share_gpu and gpus > 16:
+        return f'--share-gpu with {gpus} ranks: at most 16 processes may share a GPU'
     if world is not None:
         if int(world) != gpus:
             return f'--gpus {gpus} but WORLD_SIZE={world}: the launcher and --gpus disagree'
         return None
     if gpus == 1:
         return None
-    ndev = torch.cuda.device_count()
-    if gpus > ndev:
-        return f'--gpus {gpus} but this node has {ndev} visible GPU(s)'
+    if not share_gpu:
+        ndev = torch.cuda.device_count()
+        if gpus > ndev:
+            return f'--gpus {gpus} but this node has {ndev} visible GPU(s)'
     return 'launch'
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)')
+    ap.add_argument('--dist-backend', choices=['nccl', 'gloo'], default='nccl',
+                    help='process group backend for N > 1 (nccl = RCCL over xGMI; gloo only for '
+                         'readiness runs with --share-gpu)')
+    ap.add_argument('--share-gpu', action='store_true',
+                    help='readiness runs of the multi-rank path on a one-GPU box: every rank on '
+                         'cuda:0 (needs --dist-backend gloo; not a scaling measurement)')
     ap.add_argument('--steps', type=int, default=500)
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--preroll', type=int, default=1000,
@@ -416,7 +444,8 @@ def main():
     args = ap.parse_args()
 
     # --gpus N: N ranks, launched here if no launcher did (before any GPU call)
-    chk = check_world(args.gpus)
+    args.gpus = resolve_gpus(args.gpus)
+    chk = check_world(args.gpus, args.share_gpu, args.dist_backend)
     if chk == 'launch':
         sys.exit(launch_ranks(args.gpus))
     if chk is not None:
@@ -424,12 +453,20 @@ def main():
         sys.exit(2)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    local = 0 if args.share_gpu else int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group('gloo')
+    gloo = dist is not None and args.dist_backend == 'gloo'
+
+    def coll(t):
+        """a tensor on the process group's device (gloo: a host copy)"""
+        return t.cpu() if gloo else t
 
     from abmarl_amd import _abi
     from abmarl_amd.engine import GridWorldEngine, env_seeds
@@ -512,8 +549,8 @@ def main():
         eng.check_errors(allow=allow)
         acting = int(eng.acting.sum().item()) - acting0
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-        tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
-        kms = torch.tensor([step_ms], dtype=torch.float64, device=eng.device)
+        tot = coll(torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device))
+        kms = coll(torch.tensor([step_ms], dtype=torch.float64, device=eng.device))
         if dist:
             acts = tot.clone(); dist.all_reduce(acts, op=dist.ReduceOp.SUM)
             tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -602,8 +639,8 @@ def main():
         # launch-weighted mean: ms per launch of the full-size fragments
         full = [a.elapsed_time(b) for (i, f), (a, b) in zip(frags, evs) if f == F]
         launch_ms = float(np.mean(full))
-        tot = torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device)
-        kms = torch.tensor([launch_ms], dtype=torch.float64, device=eng.device)
+        tot = coll(torch.tensor([acting, dt, E_local], dtype=torch.float64, device=eng.device))
+        kms = coll(torch.tensor([launch_ms], dtype=torch.float64, device=eng.device))
         if dist:
             acts_t = tot.clone(); dist.all_reduce(acts_t, op=dist.ReduceOp.SUM)
             tmax = tot.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -618,7 +655,7 @@ def main():
     other = 'same_step' if mode == 'next_step' else 'next_step'
     eng, r = run(mode, rollout)
     A, n_passive = eng.A, eng.n_passive
-    stats = gather_episode_stats(eng.acting, eng.get_state()['steps'], dist)
+    stats = gather_episode_stats(coll(eng.acting), coll(eng.get_state()['steps']), dist)
     del eng
     r2 = None if (args.no_other or turn) else run(other, rollout)[1]
     # the per-step (closed-loop) protocol beside the rollout line
@@ -701,6 +738,11 @@ def main():
             'config': {'workload': workload,
                        'envs_per_gpu': E_local, 'global_envs': int(envs_all),
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
+            'dist': None if dist is None else {
+                'backend': args.dist_backend, 'ranks_share_one_gpu': bool(args.share_gpu),
+                'note': ('readiness run of the multi-rank path: every rank on cuda:0, collectives '
+                         'over gloo; NOT a scaling measurement') if args.share_gpu else
+                        'one rank per GPU'},
             'env_steps_per_s': round(envs_all * args.steps / dt_all, 1),
             'mean_acting_agents_per_env_step': round(acting_all / (envs_all * args.steps), 2),
             'acting_agent_steps': int(acting_all),

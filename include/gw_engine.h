@@ -109,7 +109,7 @@ typedef int32_t gw_status;
                                      `not attacked_agents` on the numpy array of 2 or more
                                      picks _subset_attackables returns (actor.py:412-414)
                                      raises ValueError (team_battle_example.py:41,
-                                     reach_the_target.py:107); the step stops after that
+                                     reach_the_target.py:127); the step stops after that
                                      attacker's attack (damage, ammo and draws applied)
                                      unless gw_config.attack_array_as_list              */
 
@@ -456,9 +456,13 @@ gw_status gw_component(gw_handle h, int32_t op, int32_t lane, const int32_t* arg
    step (done before it, or not grid observers) are left unwritten in that
    step's slab instead of being filled with -2 (the reference returns no obs
    for them; mask with done).  The Pacman kernel runs it in one launch too
-   (rows always written); the workgroup-per-env kernel runs it in one
-   launch with the env's state passing through HBM between its steps (rows
-   always written).
+   (rows always written).  The workgroup-per-env kernel runs it in one
+   launch too, the env's state on chip across its steps; with
+   skip_done_obs it writes only the rows of the lanes in [obs_lo, obs_hi)
+   (the contiguous range of grid-observer lanes, fixed at gw_create),
+   rounded out to whole 16-byte stores: rows of lanes that are not grid
+   observers are unspecified there, as on the one-wave kernel, and rows of
+   done observers inside the range hold -2.
    The handle's persistent obs rows (gw_config.persistent_obs) are not used. */
 gw_status gw_rollout(gw_handle h, int32_t n_steps, const int32_t* actions, int32_t* obs, double* reward,
                      uint8_t* done, uint8_t* all_done, uint8_t* all_done_in, uint64_t* acting,
@@ -593,6 +597,14 @@ int32_t     gw_num_lanes(gw_handle h);
 #define GW_KERNEL_LANE      3
 int32_t     gw_env_kernel(gw_handle h);
 int32_t     gw_act_dim(gw_handle h);
+/* Resident workgroups per CU of this engine's step launch (the HIP occupancy
+   calculator on its kernel, block size and dynamic LDS); block_threads and
+   lds_bytes (either may be NULL) receive that block size and LDS.  A launch
+   of E envs runs in ONE dispatch round when E <= blocks_per_cu * CUs (for
+   the workgroup kernel one env = one workgroup; the lane kernel packs
+   several envs per workgroup).  No reference counterpart: a diagnostic of
+   the launch shape.                                  */
+gw_status   gw_step_occupancy(gw_handle h, int32_t* blocks_per_cu, int32_t* block_threads, int64_t* lds_bytes);
 /* entity index (into gw_config.agents) of each lane; out: host int32[A]     */
 gw_status   gw_lane_entities(gw_handle h, int32_t* out);
 const char* gw_last_error(void);

@@ -12,7 +12,10 @@ import numpy as np
 from abmarl_amd import _abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, 'build', 'libgw_oracle.so')
+# GW_ORACLE_SANITIZE=1: the AddressSanitizer + UBSan build (tests/test_sanitizers.py
+# runs the golden replays on it in a child process that preloads libasan)
+SANITIZE = os.environ.get('GW_ORACLE_SANITIZE') == '1'
+LIB = os.path.join(HERE, 'build', 'asan' if SANITIZE else '', 'libgw_oracle.so')
 
 
 def build(force=False):
@@ -22,11 +25,12 @@ def build(force=False):
     srcs = [os.path.join(HERE, 'gw_oracle.c'),
             os.path.join(os.path.dirname(HERE), 'include', 'gw_engine.h')]
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    target = os.path.relpath(LIB, HERE)
     with open(LIB + '.lock', 'w') as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         if force or not os.path.exists(LIB) or \
                 os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
-            subprocess.check_call(['make', '-s', '-B' if force else '-s', '-C', HERE])
+            subprocess.check_call(['make', '-s', '-B' if force else '-s', '-C', HERE, target])
     return LIB
 
 

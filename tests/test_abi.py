@@ -76,7 +76,7 @@ def test_create_rejects_bad_config_without_gpu(lib):
     # argument validation happens before any HIP call
     h = C.c_void_p()
     assert lib.gw_create(None, 4, 0, C.byref(h)) == _abi.GW_E_INVALID
-    assert lib.gw_abi_version() == 6
+    assert lib.gw_abi_version() == 7
 
 
 def test_oracle_exports(oracle_mod):

@@ -41,3 +41,46 @@ def test_world_size_mismatch_is_refused():
     r = _bench(['--gpus', '4', '--steps', '1', '--warmup', '0'], WORLD_SIZE='2', RANK='0', LOCAL_RANK='0')
     assert r.returncode == 2, (r.returncode, r.stderr[-500:])
     assert 'disagree' in r.stderr
+
+
+def test_gpus_defaults_to_the_launchers_world(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    assert bench.resolve_gpus(None) == 1
+    monkeypatch.setenv('WORLD_SIZE', '4')
+    assert bench.resolve_gpus(None) == 4              # torchrun --nproc-per-node 4 bench.py
+    assert bench.resolve_gpus(2) == 2                 # explicit: check_world flags the mismatch
+
+
+def test_share_gpu_layouts(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    monkeypatch.setattr(bench.torch.cuda, 'device_count', lambda: 1)
+    assert bench.check_world(2, share_gpu=True, backend='gloo') == 'launch'
+    assert 'gloo' in bench.check_world(2, share_gpu=True, backend='nccl')
+    assert 'at most 16' in bench.check_world(17, share_gpu=True, backend='gloo')
+    assert 'visible GPU' in bench.check_world(2)
+
+
+def test_launcher_leaves_hip_uninitialised(monkeypatch):
+    """The launching parent of `bench.py --gpus N` starts the ranks before
+    anything initialises HIP (an exec or fork after HIP init is forbidden on
+    the GPU pool): main() reaches launch_ranks with torch.cuda uninitialised."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    seen = {}
+
+    def fake_launch(n):
+        seen['n'] = n
+        seen['init'] = bench.torch.cuda.is_initialized()
+        return 0
+    monkeypatch.setattr(bench, 'launch_ranks', fake_launch)
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '2', '--share-gpu', '--dist-backend', 'gloo',
+                                      '--steps', '1', '--warmup', '0'])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    assert seen == {'n': 2, 'init': False}

@@ -405,6 +405,13 @@ def test_reach_the_target_config4(oracle_mod):
     kw = {k: v for k, v in RTT_CONFIG4.items() if k != 'kind'}
     eng = _run_rtt(oracle_mod, kw, E=1024, T=60, horizon=25, run=4)
     assert eng.wg and eng.A == 256
+    # the 1024-env launch in ONE dispatch round on the 256 CUs: 4 resident
+    # workgroups (of 4 waves) per CU -- <= 128 VGPRs and <= 40 KiB of LDS
+    import torch
+    nblk, threads, lds = eng.step_occupancy()
+    cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
+    assert threads == 256 and lds <= 160 * 1024 // 4, (threads, lds)
+    assert nblk >= 4 and nblk * cus >= 1024, (nblk, cus)
 
 
 def test_reach_the_target_config4_all_8192_envs(oracle_mod):

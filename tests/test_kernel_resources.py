@@ -4,10 +4,12 @@ library's gfx950 code objects (AMDGPU metadata notes; CPU only).
 The launch shapes depend on them:
   * step_kernel<7, 1> (the headline) holds 4 one-wave envs per SIMD, so all
     4096 envs are resident at once on 1024 SIMDs: <= 128 VGPRs;
-  * wg_step_kernel<7> (config 4) fits 3 workgroups per CU only at <= 168
-    unified registers (512 / 3 in granules of 8): at 2 per CU the 1024-env
-    launch runs as two rounds (measured 3.83 vs 3.94 ms, 22.5 vs 30.5 ms at
-    8192 envs, profiles/r04/ab_wg_fresh_params_*.jsonl);
+  * wg_step_kernel<7> (config 4) fits 4 workgroups of 4 waves per CU at
+    <= 128 registers (with its <= 40 KiB of LDS): config 4's 1024-env share
+    of a GPU is resident in ONE dispatch round on 256 CUs.  At 159
+    registers (round 5) 3 fit and the last 256 envs ran as a second round;
+    the fixed LDS layout and the per-step opaque thread index (gw_rtt.inc
+    wg_carve / wg_fresh) took it to 123;
   * the workgroup and headline kernels touch no scratch: every scratch-using
     build of the workgroup kernel measured slower (profiles/r04/ab_wg_min_waves.txt);
   * pac_kernel runs 6 waves per SIMD (config 5: 16384 envs).
@@ -95,10 +97,35 @@ def test_headline_kernel_four_envs_per_simd(md):
     assert k['.private_segment_fixed_size'] == 0
 
 
-def test_workgroup_kernel_three_per_cu(md):
+def test_workgroup_kernel_four_per_cu(md):
     k = _get(md, r'14wg_step_kernelILi7E')
-    assert _granules(k['.vgpr_count']) <= 512 // 3, k['.vgpr_count']
+    assert _granules(k['.vgpr_count']) <= 512 // 4, k['.vgpr_count']
     assert k['.private_segment_fixed_size'] == 0
+    # static LDS + config 4's dynamic LDS (gw_rtt.inc wg_smem_bytes: 64x64,
+    # 256 lanes, S = 7, 3 encodings, 4 waves) within a quarter of 160 KiB
+    assert k['.group_segment_fixed_size'] + config4_lds_bytes() <= 160 * 1024 // 4
+
+
+def _a16(n):
+    return (n + 15) // 16 * 16
+
+
+def config4_lds_bytes(H=64, W=64, A=256, S=7, max_enc=3, nwv=4, max_lanes=256, wave=64, mt_n=624):
+    """wg_smem_bytes of gw_rtt.inc for config 4 (the fixed per-lane part,
+    the work union, the padded cell table, counts and blocker bitmap)."""
+    m_words = 64 + 3 * 64
+    lut = S * S * ((S * S + 31) // 32)
+    fixed = 6 * 4 * max_lanes + 2 * 8 * max_lanes + 4 * wave * 4 + 4 * m_words + 4 * mt_n
+    fixed = _a16(fixed + 4 * (lut if lut <= 256 else 0))
+    HW = H * W
+    cnt = _a16((HW + 3) // 4 * 4)
+    st = _a16(A * S * ((S + 3) & ~3))
+    st = max(st, 2 * cnt, _a16((max_enc + 1) * 64 * 8) + _a16(A * 4),
+             4 * 640 + 4 * mt_n + 4 * wave * nwv + 8 * (15 + 1) * 4) + 16
+    pad = S // 2                  # config 4: the target's attack range <= its view range
+    pitch = (W + 2 * pad + 3) // 4 * 4 + 4 * ((S + 3) // 4 + 1)
+    tbl = _a16((H + 2 * pad + 1) * pitch)
+    return fixed + st + tbl + cnt + _a16(((HW + 31) // 32 + 2) * 4)
 
 
 def test_pacman_kernel_six_per_simd(md):

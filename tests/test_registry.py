@@ -192,6 +192,16 @@ def test_overriding_subclass_of_a_built_in_is_refused():
         sim.compiled()
     TeamBattleSim.build_sim(5, 5, states={'SamePosition', 'HealthState'}, **kw).compiled()
 
+    # the reference's protected hooks count too (state.py:152, actor.py:394)
+    class MyPlacement(PositionState):
+        def _place_variable_position_agent(self, var_agent_to_place, **kwargs):
+            pass
+
+    register(MyPlacement)
+    sim = TeamBattleSim.build_sim(5, 5, states={'MyPlacement', 'HealthState'}, **kw)
+    with pytest.raises(UnsupportedConfig, match='overrides _place_variable_position_agent'):
+        sim.compiled()
+
 
 def test_attribute_state_twin_is_not_compiled_twice():
     """A simulation that also keeps its own PositionState attribute beside the
