@@ -65,11 +65,7 @@
 #define CELL_OFF 0xFFu
 // lane_step_kernel (gw_lane.inc): lanes per env for an S x S window (the
 // window's cell count rounded up to 16, 32 or 64; host and device)
-#ifdef GW_LANE_GROUP
-__host__ __device__ constexpr int lane_group(int) { return GW_LANE_GROUP; }
-#else
 __host__ __device__ constexpr int lane_group(int S) { return S * S <= 16 ? 16 : (S * S <= 32 ? 32 : 64); }
-#endif
 
 // create_grid_and_mask (utils.py:46-115): does a blocker at offset (rd, cd)
 // from the observer hide the cell at offset (r, c)?  The eight cases differ
@@ -252,9 +248,7 @@ __device__ __forceinline__ bool rlb(bool v, int l) { return __builtin_amdgcn_rea
 #define BUF_OOB ((int)0x80000000)
 // cache policy of the observation stores: slc (streaming, non-temporal),
 // measured -11..16% on the headline workload
-#ifndef GW_OBS_STORE_AUX
-#define GW_OBS_STORE_AUX 2
-#endif
+constexpr int GW_OBS_STORE_AUX = 2;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // four observation bytes (valid values >= -2, 0x80 = skipped) -> four int32
 // max(sext(byte), -2) with SDWA byte selects (one VALU per output), stored
@@ -409,9 +403,23 @@ __device__ __forceinline__ int select_bit(uint64_t w, uint32_t k)
         }                                                                         \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
+// sub-phase ticks summed in registers over the calls of one step (the
+// serial attackers' phases of attack_one: att_acc[k], written once to
+// stamps slots 42-48 after the attack loop, tools/stamps.py)
+#define ACC_STAMP(k, t0)                                                          \
+    do {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        const uint64_t _n = __builtin_amdgcn_s_memtime();                         \
+        if (att_acc) att_acc[(k) - 42] += _n - (t0);                              \
+        t0 = _n;                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+    } while (0)
+#define ACC_STAMP_T0(t0) uint64_t t0 = __builtin_amdgcn_s_memtime()
 #else
 #define STAMP(i) do { } while (0)
 #define STAMP_WAVE(slot, with_ids) do { } while (0)
+#define ACC_STAMP(k, t0) do { } while (0)
+#define ACC_STAMP_T0(t0) do { } while (0)
 #endif
 
 // ------------------------------------------------------------ MT19937
@@ -643,10 +651,7 @@ struct Smem {
 constexpr int JAC_WB = 160;
 // the Jacobi sweeps end without a confirming sweep when at most this many
 // estimates moved in the last one and none of them can change a fixpoint
-// (0: always confirm with a sweep)
-#ifndef GW_JAC_CONFIRM
-#define GW_JAC_CONFIRM 16
-#endif
+constexpr int GW_JAC_CONFIRM = 16;
 static_assert(JAC_WB < GW_MT_N - 397, "placement words past the twist come from the untwisted key");
 constexpr int JAC_OFF_W = 0;
 constexpr int JAC_OFF_PUB = JAC_OFF_W + 4 * JAC_WB;
@@ -1403,9 +1408,12 @@ __device__ __forceinline__ bool ammo_filter(Rng& rng, Lane& L, int a, int& nlist
 // ammo filter turned them into a list (actor.py:347-351).
 template <bool PLAIN = false>
 __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, Lane& L, int a,
-                                           int k, int& nlist, int& list, bool* ndarray = nullptr)
+                                           int k, int& nlist, int& list, bool* ndarray = nullptr,
+                                           uint64_t* att_acc = nullptr)
 {
+    (void)att_acc;
     if (ndarray) *ndarray = false;
+    ACC_STAMP_T0(t0);
     const bool BL = !PLAIN && p.blockers, LB = !PLAIN && p.lane_blockers;
     const int l = lane_id();
     nlist = 0;
@@ -1450,6 +1458,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         if (l == j) crank = rk;
     }
     const int ncand = __popcll(cm);
+    ACC_STAMP(42, t0);                                     // window scan + candidate ranks
     int rank = -1;                                         // rank among accepted
     int n = 0;
     if (acc >= 1.0) {
@@ -1468,6 +1477,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
             n++;
         }
     }
+    ACC_STAMP(43, t0);                                     // accuracy draws
     if (n == 0) return true;                                // (True, [])
     // _subset_attackables: pick (lane t) = accepted rank of list[t]
     int pick = -1;
@@ -1493,6 +1503,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         nlist = k;
         if (ndarray) *ndarray = true;
     }
+    ACC_STAMP(44, t0);                                     // subset draws
     for (int t = 0; t < nlist; t++) {
         const int pr = rl(pick, t);
         const uint64_t tm = __ballot(rank == pr);
@@ -1501,6 +1512,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
         if (l == t) list = lane_t;
     }
     if (!PLAIN && (akind & GW_K_AMMO) && ammo_filter(rng, L, a, nlist, list) && ndarray) *ndarray = false;
+    ACC_STAMP(45, t0);                                     // attacked list
     // apply damage in list order (actor.py:353-358)
     const double strength = rld(L.strength, a);
     for (int t = 0; t < nlist; t++) {
@@ -1519,6 +1531,7 @@ __device__ __forceinline__ bool attack_one(const Params& p, Smem& sm, Rng& rng, 
             table_remove(p, sm, L, b, br, bc);
         }
     }
+    ACC_STAMP(46, t0);                                     // damage + cell table
     return true;
 }
 
@@ -2221,7 +2234,6 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
             nsw++;
 #endif
             if (!any) break;
-#if GW_JAC_CONFIRM
             // Would the next sweep change anything?  Each lane's fixpoint of this
             // sweep is exact against the estimates it ranked (c = idx + #{rm
             // estimates <= c}, none of them on c), and so is its duplicate set.
@@ -2246,7 +2258,6 @@ __device__ __forceinline__ bool do_reset(const Params& p, Smem& sm, Rng& rng, La
                     if (__ballot(valid && aff) == 0) break;
                 }
             }
-#endif
         }
         if (__ballot(bad)) return 2;
         if (__ballot(ip && qbad)) { err |= GW_ERR_INIT_POSITION; return 1; }   // grid.py:81-129
@@ -2363,22 +2374,13 @@ __device__ __forceinline__ void table_template(const Params& p, Smem& sm)
 // reward[t], done[t], all_done[t] (strides E*A*act_dim, E*A*SS, E*A, E).
 // waves per SIMD the step kernel is compiled for: 4 keeps it within 128
 // VGPRs, so 16 one-wave envs (the LDS limit at TeamBattle's size) share a CU
-#ifndef GW_STEP_WAVES_PER_EU
-#define GW_STEP_WAVES_PER_EU 4
-#endif
+constexpr int GW_STEP_WAVES_PER_EU = 4;
 // a pending horizon reset counts as this many agent-steps of remaining work
 // (192 -> 384 in round 5: the driver's command median 0.2298 -> 0.2253 ms over
 // 8 alternating runs, 100-step fragments unchanged; profiles/r05/ab_prio_reset_w*.jsonl)
-#ifndef GW_PRIO_RESET_W
-#define GW_PRIO_RESET_W 384
-#endif
+constexpr int GW_PRIO_RESET_W = 384;
 // lane_step_kernel: steps of actions in flight ahead of the step (gw_lane.inc)
-#ifndef GW_LANE_PD
-#define GW_LANE_PD 4
-#endif
-#ifndef GW_STEP_SPEC
-#define GW_STEP_SPEC 1
-#endif
+constexpr int GW_LANE_PD = 4;
 // SPEC 1: the TeamBattle program without blocking entities and with one
 // view range (BASELINE's headline config): the other programs' passes and
 // the masked / mixed-range observation fold away at compile time (the
@@ -2449,6 +2451,10 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     bool lanes_in = false, need_tmpl = false;
     for (int t = 0; t < p.nsteps; t++) {
         const Params& p = kernel_params();
+#ifdef GW_AB_LAUNDER
+        int l; { l = (int)lane_id(); asm volatile("" : "+v"(l)); }
+        const bool valid = l < A;
+#endif
         // issue priority (gw_rollout): the four envs of a SIMD start together,
         // and VALU issue goes by priority, then age, so a heavy young wave
         // would trail the others and end the launch alone.  Remaining-work
@@ -2466,6 +2472,11 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             const int typ = left * 24;
             prio = rem * 4 >= typ * 6 ? 3 : (rem * 8 >= typ * 9 ? 2 : (rem * 4 >= typ * 3 ? 1 : 0));
         }
+#ifdef GW_AB_RESET_PRIO
+        else if (p.autoreset == 2 && (prev_all || (p.horizon > 0 && steps >= p.horizon))) {
+            prio = 3;
+        }
+#endif
         set_prio(prio);
         STAMP(50);
         const int32_t* act_t = p.actions + (size_t)t * EA * p.act_dim;
@@ -2546,6 +2557,11 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                 // just before the next serial attacker after them (so each lane's
                 // reward terms keep their reference order), or after the loop.
                 uint64_t pend = __ballot(att) & ~maybe_mask;
+        #ifdef GW_STAMPS
+                uint64_t att_acc[7] = {0, 0, 0, 0, 0, 0, 0};     // slots 42-47, calls (48)
+        #else
+                uint64_t* att_acc = nullptr;
+        #endif
                 // one serial attacker; `before`: the pending lanes whose turn
                 // came before a's
                 auto serial_attack = [&](int a, uint64_t before) {
@@ -2554,9 +2570,13 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                         pend &= ~before;
                     }
                     if (!rlb(L.active, a)) return;                  // killed earlier this pass
+        #ifdef GW_STAMPS
+                    att_acc[6] += 1;
+        #endif
                     int nlist, list;
                     bool nd;
-                    attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list, &nd);
+                    attack_one<PLAIN>(p, sm, rng, L, a, rl(ak, a), nlist, list, &nd, att_acc);
+                    ACC_STAMP_T0(t1);
                     // `not attacked_agents` (team_battle_example.py:41) on a numpy
                     // array of 2 or more agents raises ValueError: the step stops
                     // here, this attack applied
@@ -2571,6 +2591,7 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                             }
                         }
                     }
+                    ACC_STAMP(47, t1);                          // rewards
                 };
                 if (aord) {
                     // randomize_action_input: the action dict's order
@@ -2585,6 +2606,10 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
                     }
                 }
                 if (((pend >> l) & 1ull) && L.active) L.reward -= 0.1;
+        #ifdef GW_STAMPS
+                if (l == 0 && p.stamps)
+                    for (int q = 0; q < 7; q++) p.stamps[(size_t)e * GW_STAMP_STRIDE + 42 + q] = att_acc[q];
+        #endif
                 STAMP(2);
                 if (!raised) {
                     // ---- move pass (:50-55)
@@ -4074,7 +4099,7 @@ gw_status gw_create(const gw_config* cfg, int32_t n_envs, int32_t device, gw_han
     if (!wg && !pac) HIPCHK(set_part_attrs(g->S, PK_COMP, PK_COMP, g->smem_step, g->smem_step));
     bool any_ammo = false;
     for (int l = 0; l < A; l++) any_ammo |= (hs[l].kind & GW_K_AMMO) != 0;
-    g->step_tb = GW_STEP_SPEC && !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
+    g->step_tb = !wg && !pac && !big && p.sim_kind == GW_SIM_TEAM_BATTLE && !p.blockers && !p.lane_blockers &&
                  !p.hetero_view && !any_ammo;
     if (g->step_tb) HIPCHK(set_part_attrs(g->S, PK_STEP_TB, PK_STEP_TB, g->smem_step, g->smem_step));
     // MazeNavigation with the navigator and the target as its only lanes

@@ -197,6 +197,25 @@ def cpu_baseline(cc, seconds=10.0, envs_per_core=64, horizon=200, mode='next_ste
                       'extrapolated_all_physical_cores = per_core x every physical core of the host'))
 
 
+def _traffic(roll, pmc, envs=None):
+    """The committed PMC evidence of a launch shape (tools/prof_headline.sh
+    <tag> rtt|pacman, tools/profile.sh maze) into a quick_config rollout
+    block: HBM bytes over the algorithmic bytes of the SAME profiled launch.
+    envs: only a profile of that many envs counts (None: any)."""
+    if not os.path.exists(pmc):
+        return
+    prof = json.load(open(pmc))
+    if prof.get('algorithmic_bytes_per_launch') and prof.get('hbm_bytes_per_launch') and \
+            (envs is None or prof.get('envs') == envs):
+        roll['traffic'] = round(prof['hbm_bytes_per_launch'])
+        roll['traffic_ratio'] = round(prof['hbm_bytes_per_launch'] / prof['algorithmic_bytes_per_launch'], 4)
+        roll['traffic_source'] = f'profiles/{os.path.basename(pmc)} ({prof.get("tag")})'
+        if prof.get('traffic_ratio_calibrated'):
+            # WRITE_SIZE calibrated on the launch's own store pattern (known bytes)
+            roll['traffic_ratio_calibrated'] = round(prof['traffic_ratio_calibrated'], 4)
+            roll['write_size_calibration'] = prof['write_size_calibration']['source']
+
+
 def quick_config(name, steps=200, warmup=400):
     """A short single-GPU measurement of another BASELINE config (not the
     metric's): agent-steps/s and the step kernel's average launch time, after
@@ -265,6 +284,7 @@ def quick_config(name, steps=200, warmup=400):
                 'launch_ms': round(lms, 4), 'steps_per_launch': F, 'bytes_per_launch': round(rb),
                 'achieved_GBs': round(rb / (lms * 1e-3) / 1e9, 2),
                 'protocol': 'gw_turn_rollout fragments (one launch per 50 turns) on actions resident in HBM'}
+        _traffic(roll, os.path.join(ROOT, 'profiles', f'pmc_pac_kernel_rollout_f{F}.json'), envs=E)
     else:
         # the same engine as gw_rollout fragments of 100 steps on actions
         # resident in HBM (the headline line's protocol)
@@ -300,17 +320,8 @@ def quick_config(name, steps=200, warmup=400):
                 'protocol': 'gw_rollout fragments of 100 steps on actions resident in HBM (after an '
                             'untimed first fragment), launch events recorded by the dispatch'}
         kn = {'maze': 'lane_step_kernel', 'rtt': 'wg_step_kernel', 'rtt_8192': 'wg_step_kernel'}[name]
-        pmc = os.path.join(ROOT, 'profiles', f'pmc_{kn}_rollout_f{F}.json')
-        if os.path.exists(pmc):
-            # the committed PMC evidence of this launch shape (tools/prof_headline.sh
-            # <tag> rtt, tools/profile.sh maze): HBM bytes over the algorithmic
-            # bytes of the SAME profiled launch
-            prof = json.load(open(pmc))
-            if prof.get('algorithmic_bytes_per_launch') and prof.get('hbm_bytes_per_launch') and \
-                    (name != 'rtt_8192' or prof.get('envs') == 8192):
-                roll['traffic'] = round(prof['hbm_bytes_per_launch'])
-                roll['traffic_ratio'] = round(prof['hbm_bytes_per_launch'] / prof['algorithmic_bytes_per_launch'], 4)
-                roll['traffic_source'] = f'profiles/{os.path.basename(pmc)} ({prof.get("tag")})'
+        _traffic(roll, os.path.join(ROOT, 'profiles', f'pmc_{kn}_rollout_f{F}.json'),
+                 envs=8192 if name == 'rtt_8192' else None)
     if name == 'maze':
         nbytes = step_bytes(E, eng.A, cc.obs_side)
         desc = ('MazeNavigation 16x16 (workloads.MAZE_16), 1024 envs, AllStep, next_step auto-reset '
@@ -694,7 +705,7 @@ def main():
         # rollout profile is per fragment length: tools/profile.sh ... <F>)
         pmc = os.path.join(ROOT, 'profiles', f'pmc_{kname.split("<")[0]}{f"_rollout_f{F}" if rollout else ""}.json')
         prof = {}
-        if args.workload in ('team_battle', 'maze', 'rtt') and not args.workgroup_waves and os.path.exists(pmc):
+        if args.workload in ('team_battle', 'maze', 'rtt', 'pacman') and not args.workgroup_waves and os.path.exists(pmc):
             prof = json.load(open(pmc))
             traffic = prof.get('hbm_bytes_per_launch')
             rocprof_ms = prof.get('rocprof_avg_ms')
@@ -737,6 +748,7 @@ def main():
             'data': 'synthetic: Philox random-policy actions, random-init episodes',
             'config': {'workload': workload,
                        'envs_per_gpu': E_local, 'global_envs': int(envs_all),
+                       'lanes': A, 'passive_entities': n_passive, 'cells': cc.rows * cc.cols,
                        'parallelism': f'env-sharded x{world} (no data-path collective)'},
             'dist': None if dist is None else {
                 'backend': args.dist_backend, 'ranks_share_one_gpu': bool(args.share_gpu),

@@ -3,7 +3,9 @@
 # own workload (bench.py --gpus 1 --steps 20 --warmup 5: 1000-step pre-roll,
 # ONE timed 20-step gw_rollout launch):
 #   bash tools/prof_headline.sh <tag> [rtt]   -> gpurun_out/ph_<tag>/
-# (rtt: BASELINE config 4's line, bench.py --workload rtt --steps 100 --warmup 5)
+# (rtt: BASELINE config 4's line, bench.py --workload rtt --steps 100 --warmup 5;
+#  pacman: config 5's turn rollout, --workload pacman --steps 50 --warmup 5,
+#  ONE timed 50-turn gw_turn_rollout launch)
 # 1. --kernel-trace --stats over the driver's exact command;
 # 2. FETCH_SIZE and WRITE_SIZE, one --pmc pass each, same workload with the
 #    other configs and the CPU baseline skipped (--no-other --no-cpu-baseline:
@@ -20,6 +22,8 @@ export TMPDIR=/tmp
 WL=${2:-team_battle}
 if [ "$WL" = rtt ]; then
   CMD="python3 bench.py --gpus 1 --workload rtt --steps 100 --warmup 5"
+elif [ "$WL" = pacman ]; then
+  CMD="python3 bench.py --gpus 1 --workload pacman --steps 50 --warmup 5"
 else
   CMD="python3 bench.py --gpus 1 --steps 20 --warmup 5"
 fi

@@ -112,6 +112,17 @@ def main():
               f'(max {ns.max()}); attack ticks per such attacker: median {np.median(at[ok] / ns[ok]):.0f}')
         print(f'movers per env: median {np.median(st[:, 31]):.0f}, not isolated (serial) median '
               f'{np.median(st[:, 30]):.0f} max {st[:, 30].max()}')
+        cnt = st[:, 48]
+        if cnt.sum() > 0:
+            okc = cnt > 0
+            print(f'serial attack_one calls: {int(cnt.sum())} in {okc.sum()} envs; per call (sum over envs / calls), '
+                  f'median of per-env means:')
+            for k, nm in zip(range(42, 48), ['window scan + ranks', 'accuracy draws', 'subset draws',
+                                             'attacked list', 'damage + cell table', 'rewards']):
+                per_env = st[okc, k] / cnt[okc]
+                print(f'   {nm:>22}: {st[:, k].sum() / cnt.sum():8.0f}   median {np.median(per_env):8.0f}')
+            loop = (st[:, 2] - st[:, 7])
+            print(f'   {"loop total / call":>22}: {loop[okc].sum() / cnt.sum():8.0f}')
         for lo, hi in [(0, 4), (4, 8), (8, 16), (16, 64)]:
             m = (ns >= lo) & (ns < hi)
             if m.any():

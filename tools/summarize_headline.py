@@ -18,6 +18,10 @@ dispatches are [100] * 9 + [85, 20] and then the timed one (index 11).
 --workload rtt: the same for BASELINE config 4's line (bench.py --workload
 rtt --steps 100 --warmup 5: wg_step_kernel<7>, 1024 envs, one timed 100-step
 launch; <tag>_rtt_* and pmc_wg_step_kernel_rollout_f100.json).
+--workload pacman: config 5 (bench.py --workload pacman --steps 50 --warmup
+5: pac_kernel<4>, 16384 envs, one timed 50-turn gw_turn_rollout launch;
+<tag>_pacman_* and pmc_pac_kernel_rollout_f50.json; algorithmic bytes =
+bench.pacman_turn_rollout_bytes of that launch).
 
 usage: python tools/summarize_headline.py <tag> --raw DIR --dest DIR [--workload rtt]
 """
@@ -36,6 +40,9 @@ sys.path.insert(0, ROOT)
 WORKLOADS = {
     'team_battle': ('step_kernel<7, 1>', 4096, 64, 7, 20, 3, '--gpus 1 --steps 20 --warmup 5'),
     'rtt': ('wg_step_kernel<7>', 1024, 256, 7, 100, 11, '--gpus 1 --workload rtt --steps 100 --warmup 5'),
+    # config 5: pac_kernel<PAC_STEP_TURN>, one timed 50-turn gw_turn_rollout
+    # (lanes and food words from the bench line's config)
+    'pacman': ('pac_kernel<4>', 16384, None, None, 50, 2, '--gpus 1 --workload pacman --steps 50 --warmup 5'),
 }
 KERNEL = 'step_kernel<7, 1>'
 E, A, S, F, ACT_DIM = 4096, 64, 7, 20, 3
@@ -131,8 +138,19 @@ def main():
                 p[k] = v
     pl = bench_line(os.path.join(a.raw, 'p1.log'))
     acting = pl['acting_agent_steps']
-    alg = rollout_bytes(E, A, S, F, acting, ACT_DIM)
-    alg_writes = F * E * (A * (8 + 1) + 1) + 4 * S * S * acting + E * A * (8 + 4 + 8 + 1) + E * 41
+    if a.workload == 'pacman':
+        from bench import pacman_turn_rollout_bytes
+        A = pl['config']['lanes']
+        pw = (pl['config']['passive_entities'] + 31) // 32
+        HW = pl['config']['cells']
+        # every acting agent-step returns one observation row (bench.py)
+        alg = pacman_turn_rollout_bytes(E, A, HW, pw, F, acting)
+        alg_writes = F * E * (A * (8 + 1 + 1) + 1 + 4) + 4 * HW * acting + E * (A * 29 + 4 * pw + 4 + 4 + 8 + 8)
+        rb = 'bench.pacman_turn_rollout_bytes'
+    else:
+        alg = rollout_bytes(E, A, S, F, acting, ACT_DIM)
+        alg_writes = F * E * (A * (8 + 1) + 1) + 4 * S * S * acting + E * A * (8 + 4 + 8 + 1) + E * 41
+        rb = 'bench.rollout_bytes'
     fetch = p['FETCH_SIZE'][ti] * 1024.0
     write = p['WRITE_SIZE'][ti] * 1024.0
     hbm = 2.0 * fetch + write
@@ -178,8 +196,8 @@ def main():
           f'- resources: `{res}`', '',
           '## Traffic of the timed launch (PMC run)', '',
           f'- acting agent-steps in the launch: {acting}',
-          f'- algorithmic bytes (bench.rollout_bytes): {alg / 1e6:.2f} MB '
-          f'({alg / acting:.1f} B per acting agent-step; SURVEY §8d counts 251)',
+          f'- algorithmic bytes ({rb}): {alg / 1e6:.2f} MB '
+          f'({alg / acting:.1f} B per acting agent-step)',
           f'- FETCH_SIZE {fetch / 1e6:.2f} MB raw, x2 gfx950 correction {2 * fetch / 1e6:.2f} MB; '
           f'WRITE_SIZE {write / 1e6:.2f} MB (algorithmic writes {alg_writes / 1e6:.2f} MB: '
           f'ratio {write / alg_writes:.3f})',
