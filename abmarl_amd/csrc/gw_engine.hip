@@ -2451,10 +2451,6 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
     bool lanes_in = false, need_tmpl = false;
     for (int t = 0; t < p.nsteps; t++) {
         const Params& p = kernel_params();
-#ifdef GW_AB_LAUNDER
-        int l; { l = (int)lane_id(); asm volatile("" : "+v"(l)); }
-        const bool valid = l < A;
-#endif
         // issue priority (gw_rollout): the four envs of a SIMD start together,
         // and VALU issue goes by priority, then age, so a heavy young wave
         // would trail the others and end the launch alone.  Remaining-work
