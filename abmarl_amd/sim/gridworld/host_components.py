@@ -69,10 +69,10 @@ class _HostAttackActor(AttackActorBaseComponent):
         return np.random.choice(attackable_agents, size=number_of_attacks, replace=self.stacked_attacks)
 
     def _window(self, agent):
-        """(cells, visible) of the attack range: row-major (r, c) of the
-        visible in-grid cells and the local grid."""
-        local, mask = create_grid_and_mask(agent, self.grid, agent.attack_range, self.agents)
-        return local, mask
+        """(local grid, visibility mask) of the attacker's attack range
+        (create_grid_and_mask: cells are dicts or None off the grid, mask 0
+        behind an active blocking agent)."""
+        return create_grid_and_mask(agent, self.grid, agent.attack_range, self.agents)
 
 
 class EncodingBasedAttackActor(_HostAttackActor):
