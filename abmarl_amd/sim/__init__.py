@@ -1,2 +1,2 @@
 from abmarl_amd.sim.agent_based_simulation import (  # noqa: F401
-    PrincipleAgent, ActingAgent, ObservingAgent, Agent, AgentBasedSimulation)
+    PrincipleAgent, ActingAgent, ObservingAgent, Agent, AgentBasedSimulation, DynamicOrderSimulation)

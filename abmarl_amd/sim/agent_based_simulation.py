@@ -5,6 +5,7 @@ abmarl/sim/agent_based_simulation.py (PrincipleAgent :7-63, ActingAgent :66-117,
 ObservingAgent :120-171, Agent :174-186, AgentBasedSimulation :189-294).
 """
 from abc import ABC, abstractmethod
+from collections.abc import Container
 
 from abmarl_amd import spaces as sp
 from abmarl_amd.sim import host_version
@@ -186,3 +187,23 @@ class AgentBasedSimulation(ABC):
     @abstractmethod
     def get_info(self, agent_id, **kwargs):
         pass
+
+
+class DynamicOrderSimulation(AgentBasedSimulation):
+    """A simulation that decides whose turn comes next as it runs
+    (reference: abmarl/sim/agent_based_simulation.py:297-317): next_agent is
+    one agent id or a container of them, every one an agent of the sim; a
+    single id is held as a one-element list."""
+
+    @property
+    def next_agent(self):
+        return self._next_agent
+
+    @next_agent.setter
+    def next_agent(self, value):
+        assert isinstance(value, (str, Container)), \
+            "next_agent takes an agent id or a container of agent ids."
+        ids = [value] if type(value) is str else value
+        assert all(aid in self.agents for aid in ids), \
+            "Each next agent must be one of the simulation's agents."
+        self._next_agent = ids
