@@ -2468,11 +2468,6 @@ __global__ __launch_bounds__(WAVE, GW_STEP_WAVES_PER_EU) void step_kernel(Params
             const int typ = left * 24;
             prio = rem * 4 >= typ * 6 ? 3 : (rem * 8 >= typ * 9 ? 2 : (rem * 4 >= typ * 3 ? 1 : 0));
         }
-#ifdef GW_AB_RESET_PRIO
-        else if (p.autoreset == 2 && (prev_all || (p.horizon > 0 && steps >= p.horizon))) {
-            prio = 3;
-        }
-#endif
         set_prio(prio);
         STAMP(50);
         const int32_t* act_t = p.actions + (size_t)t * EA * p.act_dim;
